@@ -1,0 +1,132 @@
+/*
+ * plenum_verify.h — C ABI of the MI355X batch signature-verification and
+ * vote-tally engine (libplenum_verify.so).
+ *
+ * Drop-in boundary for Plenum's request-authentication hot path.  Each entry
+ * point names the reference interface it replaces:
+ *
+ *   pv_verify_batch  replaces N calls of libnacl.crypto_sign_open(sig||msg, pk)
+ *                    made by stp_core/crypto/nacl_wrappers.py:86-108
+ *                    (VerifyKey.verify) via Verifier.verify (:232-242) and
+ *                    plenum/common/verifier.py:53-54 (DidVerifier.verify).
+ *                    Native side of that call: libsodium 1.0.18
+ *                    int crypto_sign_open(unsigned char *m, unsigned long long *mlen_p,
+ *                                         const unsigned char *sm, unsigned long long smlen,
+ *                                         const unsigned char *pk);
+ *                    (/opt/conda/include/sodium/crypto_sign.h:67).  Verdicts are
+ *                    bit-exact with crypto_sign_ed25519_verify_detached on
+ *                    (sig[0:64], msg).  The sig||msg framing (smlen < 64 rejects,
+ *                    a non-64-byte decoded signature shifts bytes into M) is the
+ *                    caller's job, exactly as in the reference;
+ *                    the Python glue (plenum_gpu.nacl_wrappers) does it.
+ *   pv_tally         replaces the per-3PC-batch voter-set count of
+ *                    plenum/server/models.py:16-114 (Commits/Prepares.addVote +
+ *                    hasQuorum) with quorum values from plenum/server/quorums.py:15-39.
+ *   pv_sign_batch    batch counterpart of SigningKey(seed) + sign
+ *                    (stp_core/crypto/nacl_wrappers.py:130-176; crypto_sign_seed_keypair
+ *                    + crypto_sign_detached).  Used to generate fixtures/bench data.
+ *
+ * Conventions:
+ *   - All host buffers are owned by the caller; nothing is retained after return.
+ *   - Return 0 on success, a negative errno-style code on failure; no exceptions
+ *     cross the ABI.  pv_last_error() describes the last failure (thread-local).
+ *   - Calls are synchronous and thread-compatible (one caller thread at a time per
+ *     device set), matching the single Looper thread (stp_core/loop/looper.py:64).
+ *   - A verdict is a pure function of (pk, sig64, M).
+ *   - msg_off has n+1 entries; message i is msg_blob[msg_off[i] : msg_off[i+1]].
+ *
+ * Device-pointer variants (*_device) take device pointers on `device` and an
+ * optional hipStream_t (NULL = a library-owned stream) and return after the
+ * work is enqueued AND complete (they synchronise the stream).  The message
+ * blob passed to a device variant must have >= 16 readable bytes after the last
+ * message (the hash kernel reads aligned words).
+ */
+#ifndef PLENUM_VERIFY_H
+#define PLENUM_VERIFY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PV_OK 0
+#define PV_EINVAL (-22)   /* bad argument */
+#define PV_ENODEV (-19)   /* no usable GPU in device_mask */
+#define PV_ENOMEM (-12)   /* device allocation failed */
+#define PV_EIO (-5)       /* HIP runtime / kernel failure */
+#define PV_ENOTINIT (-77) /* pv_init not called */
+
+/* flags for pv_verify_batch */
+#define PV_FLAG_NONE 0u
+
+/* Initialise the engine on the GPUs in device_mask (bit d = HIP device d;
+ * 0 = all visible devices).  Idempotent.  Builds the base-point table. */
+int pv_init(uint32_t device_mask);
+
+/* Release every device resource.  Safe to call when not initialised. */
+void pv_shutdown(void);
+
+/* Human-readable description of the last error on this thread ("" if none). */
+const char *pv_last_error(void);
+
+/* Number of devices the engine is using (after pv_init), else 0. */
+int pv_device_count(void);
+
+/* Verify n signatures held in HOST memory.
+ *   pk      n x 32 bytes
+ *   sig     n x 64 bytes (R || S; the first 64 bytes of sig||msg)
+ *   msg_blob, msg_off  messages (see conventions)
+ *   verdict n bytes out, 1 = valid, 0 = invalid
+ * The batch is split into contiguous shards over the devices in device_mask
+ * (0 = every initialised device). */
+int pv_verify_batch(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
+                    uint64_t n, uint8_t *verdict, uint32_t device_mask, uint32_t flags);
+
+/* Same with DEVICE pointers on `device`.  msg_off entries are offsets into
+ * msg_blob.  bitmap (may be NULL) receives ceil(n/64) 64-bit words: bit i%64 of
+ * word i/64 = verdict i (the layout all-gathered across ranks). */
+int pv_verify_batch_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
+                           uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device, void *stream);
+
+/* Per-batch quorum tally (HOST memory).
+ *   verdict    n_msgs bytes (1 = vote counts)
+ *   sender     n_msgs node indices (< n_nodes <= 1024)
+ *   batch_off  n_batches + 1 offsets into verdict/sender
+ *   votes      n_batches out: distinct valid senders per batch
+ *   reached    n_batches out: votes >= quorum
+ * Duplicate senders count once (a voter SET, plenum/server/models.py:24-28). */
+int pv_tally(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off, uint64_t n_batches,
+             uint32_t n_nodes, uint32_t quorum, uint32_t *votes, uint8_t *reached);
+
+int pv_tally_device(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off, uint64_t n_batches,
+                    uint32_t n_nodes, uint32_t quorum, uint32_t *votes, uint8_t *reached, int device, void *stream);
+
+/* Batch keygen + sign (HOST memory): pk_out[i], sig_out[i] for seed i over
+ * message i.  Deterministic (RFC 8032 / crypto_sign_detached). */
+int pv_sign_batch(const uint8_t *seeds, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n,
+                  uint8_t *pk_out, uint8_t *sig_out);
+
+int pv_sign_batch_device(const uint8_t *seeds, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n,
+                         uint8_t *pk_out, uint8_t *sig_out, int device, void *stream);
+
+/* Deterministic synthetic workload on the device (bench/tests; spec in
+ * plenum_gpu/synth.py): fixed-length messages, seeds, tamper flags, signed,
+ * tampered.  Outputs are device buffers the caller allocated:
+ *   off (n+1), blob (n*mlen + 16), seeds (n*32), pk (n*32), sig (n*64), tamper (n). */
+int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen, uint64_t *off,
+                    uint8_t *blob, uint8_t *seeds, uint8_t *pk, uint8_t *sig, uint8_t *tamper, int device,
+                    void *stream);
+
+/* Time the verify kernels alone over `iters` launches on device-resident
+ * inputs using HIP events on the launch stream; returns per-kernel average
+ * milliseconds (hash, curve). */
+int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
+                          uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device, void *stream, int iters,
+                          float *ms_hash, float *ms_curve);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLENUM_VERIFY_H */

@@ -1,0 +1,80 @@
+"""Build libplenum_verify.so (HIP, gfx950) in-tree.
+
+    python indy-plenum_amd/build.py            # build if sources changed
+    python indy-plenum_amd/build.py --force
+
+Output: indy-plenum_amd/lib/libplenum_verify.so (git-ignored, travels to the
+GPU box with the gpurun snapshot).  Compiles on a CPU-only host: hipcc
+cross-compiles gfx950 code objects.
+"""
+import argparse
+import hashlib
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, 'csrc')
+LIBDIR = os.path.join(HERE, 'lib')
+LIB = os.path.join(LIBDIR, 'libplenum_verify.so')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = 'gfx950'
+SOURCES = ['pv_kernels.hip', 'pv_api.cpp']
+COMMON = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-Wall', '-Wno-unused-function',
+          '-Wno-unused-variable', '-I' + os.path.join(REPO, 'include')]
+
+
+def _digest():
+    h = hashlib.sha256()
+    for fn in sorted(os.listdir(CSRC)):
+        with open(os.path.join(CSRC, fn), 'rb') as fh:
+            h.update(fn.encode() + fh.read())
+    with open(os.path.join(REPO, 'include', 'plenum_verify.h'), 'rb') as fh:
+        h.update(fh.read())
+    h.update(' '.join(COMMON).encode())
+    return h.hexdigest()
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError('build failed:\n' + ' '.join(cmd) + '\n' + r.stdout + r.stderr)
+    return r.stdout + r.stderr
+
+
+def build(force=False, verbose=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    stamp = LIB + '.stamp'
+    dig = _digest()
+    if not force and os.path.exists(LIB) and os.path.exists(stamp):
+        with open(stamp) as fh:
+            if fh.read().strip() == dig:
+                return LIB
+    objs = []
+    cmds = []
+    for src in SOURCES:
+        obj = os.path.join(LIBDIR, src + '.o')
+        lang = ['-x', 'hip'] if src.endswith('.hip') else []
+        cmds.append([HIPCC] + COMMON + lang + ['-c', os.path.join(CSRC, src), '-o', obj])
+        objs.append(obj)
+    with ThreadPoolExecutor(len(cmds)) as ex:
+        for out in ex.map(_run, cmds):
+            if verbose and out.strip():
+                print(out)
+    tmp = LIB + '.tmp'
+    _run([HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', tmp] + objs)
+    os.replace(tmp, LIB)
+    with open(stamp, 'w') as fh:
+        fh.write(dig)
+    return LIB
+
+
+if __name__ == '__main__':
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--force', action='store_true')
+    ap.add_argument('-v', '--verbose', action='store_true')
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=a.verbose))
+    sys.exit(0)

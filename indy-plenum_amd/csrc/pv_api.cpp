@@ -1,0 +1,382 @@
+// C-ABI layer of libplenum_verify.so (include/plenum_verify.h).
+//
+// Owns per-device state (stream, base-point table, workspaces), shards host
+// batches over the devices in a mask (contiguous index ranges, SURVEY.md
+// §8(e)), and launches the kernels in pv_kernels.hip.  No exceptions cross
+// the ABI: every entry point returns 0 or a negative code and records a
+// message for pv_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/plenum_verify.h"
+#include "pv_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_OK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      return fail(e_ == hipErrorOutOfMemory ? PV_ENOMEM : PV_EIO, "%s failed: %s (%s:%d)", #expr, \
+                  hipGetErrorString(e_), __FILE__, __LINE__);                                 \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  hipError_t ensure(size_t n) {
+    if (n <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n < 64 ? 64 : n;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Device {
+  int id = -1;
+  hipStream_t stream = nullptr;
+  int cu_count = 0;
+  int curve_blocks = 0;
+  DevBuf<uint32_t> btab;
+  DevBuf<uint32_t> scratch;   // per-lane A tables for the persistent curve grid
+  DevBuf<uint32_t> h;         // 8 words per signature
+  DevBuf<uint8_t> pre;
+  // staging for host-memory calls
+  DevBuf<uint8_t> pk, sig, blob, verdict, tamper;
+  DevBuf<uint64_t> off, bitmap, batch_off;
+  DevBuf<uint32_t> sender, votes;
+  DevBuf<uint8_t> reached;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+std::mutex g_mu;
+std::vector<Device> g_devs;
+
+Device* find_dev(int id) {
+  for (auto& d : g_devs)
+    if (d.id == id) return &d;
+  return nullptr;
+}
+
+int init_device(Device& d) {
+  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, d.id));
+  d.cu_count = prop.multiProcessorCount;
+  HIP_OK(d.btab.ensure(pv::BTAB_ENTRIES * pv::BTAB_WORDS));
+  HIP_OK(pv::launch_btable_init(d.btab.p, d.stream));
+  // persistent curve grid: resident blocks per CU from the occupancy query
+  // (kept <= 4 blocks of 256 threads per CU, see cdna_hip_programming.md §1)
+  int per_cu = 0;
+  HIP_OK(pv::curve_occupancy(&per_cu));
+  if (per_cu < 1) per_cu = 1;
+  if (per_cu > 4) per_cu = 4;
+  d.curve_blocks = d.cu_count * per_cu;
+  HIP_OK(d.scratch.ensure((size_t)d.curve_blocks * pv::CURVE_BLOCK * pv::ATAB_WORDS));
+  for (auto& e : d.ev) HIP_OK(hipEventCreate(&e));
+  HIP_OK(hipStreamSynchronize(d.stream));
+  return PV_OK;
+}
+
+void release_device(Device& d) {
+  if (d.id < 0) return;
+  (void)hipSetDevice(d.id);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  d.btab.release(); d.scratch.release(); d.h.release(); d.pre.release();
+  d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
+  d.off.release(); d.bitmap.release(); d.batch_off.release();
+  d.sender.release(); d.votes.release(); d.reached.release();
+  for (auto& e : d.ev)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+  d.stream = nullptr;
+  d.id = -1;
+}
+
+// enqueue hash + curve for device-resident inputs on stream s
+int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                   uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed, float* ms_hash,
+                   float* ms_curve) {
+  if (n == 0) return PV_OK;
+  HIP_OK(d.h.ensure(n * 8));
+  HIP_OK(d.pre.ensure(n));
+  uint64_t* bm = bitmap;
+  if (!bm) {
+    HIP_OK(d.bitmap.ensure((n + 63) / 64));
+    bm = d.bitmap.p;
+  }
+  if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
+  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.h.p, d.pre.p, s));
+  if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
+  HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict, bm,
+                          n, d.curve_blocks, s));
+  if (timed) {
+    HIP_OK(hipEventRecord(d.ev[2], s));
+    HIP_OK(hipEventSynchronize(d.ev[2]));
+    float a = 0, b = 0;
+    HIP_OK(hipEventElapsedTime(&a, d.ev[0], d.ev[1]));
+    HIP_OK(hipEventElapsedTime(&b, d.ev[1], d.ev[2]));
+    if (ms_hash) *ms_hash += a;
+    if (ms_curve) *ms_curve += b;
+  }
+  return PV_OK;
+}
+
+std::vector<Device*> select_devs(uint32_t mask) {
+  std::vector<Device*> v;
+  for (auto& d : g_devs)
+    if (mask == 0 || (mask >> d.id) & 1u) v.push_back(&d);
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pv_init(uint32_t device_mask) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) return fail(PV_ENODEV, "no HIP device available (%s)", hipGetErrorString(e));
+  for (int id = 0; id < count && id < 32; ++id) {
+    if (device_mask && !((device_mask >> id) & 1u)) continue;
+    if (find_dev(id)) continue;
+    g_devs.emplace_back();
+    g_devs.back().id = id;
+    int rc = init_device(g_devs.back());
+    if (rc != PV_OK) {
+      release_device(g_devs.back());
+      g_devs.pop_back();
+      return rc;
+    }
+  }
+  if (g_devs.empty()) return fail(PV_ENODEV, "device_mask 0x%x selects no visible device", device_mask);
+  return PV_OK;
+}
+
+void pv_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& d : g_devs) release_device(d);
+  g_devs.clear();
+}
+
+const char* pv_last_error(void) { return g_err.c_str(); }
+
+int pv_device_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return (int)g_devs.size();
+}
+
+int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off,
+                    uint64_t n, uint8_t* verdict, uint32_t device_mask, uint32_t flags) {
+  (void)flags;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (n == 0) return PV_OK;
+  if (!pk || !sig || !msg_off || !verdict || (!msg_blob && msg_off[n] != msg_off[0]))
+    return fail(PV_EINVAL, "null buffer");
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return fail(PV_EINVAL, "msg_off not monotone at %llu", (unsigned long long)i);
+  std::vector<Device*> devs = select_devs(device_mask);
+  if (devs.empty()) return fail(PV_ENODEV, "device_mask 0x%x selects no initialised device", device_mask);
+  const uint64_t G = devs.size();
+  std::vector<std::vector<uint64_t>> offs(G);
+  // enqueue every shard, then drain
+  for (uint64_t g = 0; g < G; ++g) {
+    Device& d = *devs[g];
+    const uint64_t s = n * g / G, e = n * (g + 1) / G, m = e - s;
+    if (m == 0) continue;
+    HIP_OK(hipSetDevice(d.id));
+    const uint64_t b0 = msg_off[s], bytes = msg_off[e] - b0;
+    offs[g].resize(m + 1);
+    for (uint64_t k = 0; k <= m; ++k) offs[g][k] = msg_off[s + k] - b0;
+    HIP_OK(d.pk.ensure(m * 32));
+    HIP_OK(d.sig.ensure(m * 64));
+    HIP_OK(d.blob.ensure(bytes + 16));
+    HIP_OK(d.off.ensure(m + 1));
+    HIP_OK(d.verdict.ensure(m));
+    HIP_OK(hipMemcpyAsync(d.pk.p, pk + 32 * s, m * 32, hipMemcpyHostToDevice, d.stream));
+    HIP_OK(hipMemcpyAsync(d.sig.p, sig + 64 * s, m * 64, hipMemcpyHostToDevice, d.stream));
+    if (bytes) HIP_OK(hipMemcpyAsync(d.blob.p, msg_blob + b0, bytes, hipMemcpyHostToDevice, d.stream));
+    HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.stream));
+    HIP_OK(hipMemcpyAsync(d.off.p, offs[g].data(), (m + 1) * 8, hipMemcpyHostToDevice, d.stream));
+    int rc = enqueue_verify(d, d.pk.p, d.sig.p, d.blob.p, d.off.p, m, d.verdict.p, nullptr, d.stream, false, nullptr,
+                            nullptr);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(verdict + s, d.verdict.p, m, hipMemcpyDeviceToHost, d.stream));
+  }
+  for (uint64_t g = 0; g < G; ++g) {
+    HIP_OK(hipSetDevice(devs[g]->id));
+    HIP_OK(hipStreamSynchronize(devs[g]->stream));
+  }
+  return PV_OK;
+}
+
+int pv_verify_batch_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off,
+                           uint64_t n, uint8_t* verdict, uint64_t* bitmap, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n == 0) return PV_OK;
+  if (!pk || !sig || !msg_blob || !msg_off || !verdict) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_time_verify_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off,
+                          uint64_t n, uint8_t* verdict, uint64_t* bitmap, int device, void* stream, int iters,
+                          float* ms_hash, float* ms_curve) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (iters <= 0) return fail(PV_EINVAL, "iters must be > 0");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  float a = 0, b = 0;
+  for (int it = 0; it < iters; ++it) {
+    int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, true, &a, &b);
+    if (rc) return rc;
+  }
+  if (ms_hash) *ms_hash = a / iters;
+  if (ms_curve) *ms_curve = b / iters;
+  return PV_OK;
+}
+
+int pv_tally_device(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
+                    uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n_nodes == 0 || n_nodes > 1024) return fail(PV_EINVAL, "n_nodes must be in 1..1024");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(pv::launch_tally(verdict, sender, batch_off, n_batches, n_nodes, quorum, votes, reached, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
+             uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (n_nodes == 0 || n_nodes > 1024) return fail(PV_EINVAL, "n_nodes must be in 1..1024");
+  if (n_batches == 0) return PV_OK;
+  if (!verdict || !sender || !batch_off || !votes || !reached) return fail(PV_EINVAL, "null buffer");
+  Device& d = g_devs[0];
+  HIP_OK(hipSetDevice(d.id));
+  const uint64_t b0 = batch_off[0], m = batch_off[n_batches] - b0;
+  std::vector<uint64_t> offs(n_batches + 1);
+  for (uint64_t k = 0; k <= n_batches; ++k) {
+    if (k && batch_off[k] < batch_off[k - 1]) return fail(PV_EINVAL, "batch_off not monotone");
+    offs[k] = batch_off[k] - b0;
+  }
+  HIP_OK(d.verdict.ensure(m ? m : 1));
+  HIP_OK(d.sender.ensure(m ? m : 1));
+  HIP_OK(d.batch_off.ensure(n_batches + 1));
+  HIP_OK(d.votes.ensure(n_batches));
+  HIP_OK(d.reached.ensure(n_batches));
+  if (m) {
+    HIP_OK(hipMemcpyAsync(d.verdict.p, verdict + b0, m, hipMemcpyHostToDevice, d.stream));
+    HIP_OK(hipMemcpyAsync(d.sender.p, sender + b0, m * 4, hipMemcpyHostToDevice, d.stream));
+  }
+  HIP_OK(hipMemcpyAsync(d.batch_off.p, offs.data(), (n_batches + 1) * 8, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(pv::launch_tally(d.verdict.p, d.sender.p, d.batch_off.p, n_batches, n_nodes, quorum, d.votes.p, d.reached.p,
+                          d.stream));
+  HIP_OK(hipMemcpyAsync(votes, d.votes.p, n_batches * 4, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipMemcpyAsync(reached, d.reached.p, n_batches, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipStreamSynchronize(d.stream));
+  return PV_OK;
+}
+
+int pv_sign_batch_device(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n,
+                         uint8_t* pk_out, uint8_t* sig_out, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n == 0) return PV_OK;
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(pv::launch_sign(seeds, msg_blob, msg_off, n, d->btab.p, pk_out, sig_out, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_sign_batch(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n,
+                  uint8_t* pk_out, uint8_t* sig_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (n == 0) return PV_OK;
+  if (!seeds || !msg_off || !pk_out || !sig_out) return fail(PV_EINVAL, "null buffer");
+  Device& d = g_devs[0];
+  HIP_OK(hipSetDevice(d.id));
+  const uint64_t b0 = msg_off[0], bytes = msg_off[n] - b0;
+  std::vector<uint64_t> offs(n + 1);
+  for (uint64_t k = 0; k <= n; ++k) offs[k] = msg_off[k] - b0;
+  HIP_OK(d.tamper.ensure(n * 32));  // seeds staging
+  HIP_OK(d.blob.ensure(bytes + 16));
+  HIP_OK(d.off.ensure(n + 1));
+  HIP_OK(d.pk.ensure(n * 32));
+  HIP_OK(d.sig.ensure(n * 64));
+  HIP_OK(hipMemcpyAsync(d.tamper.p, seeds, n * 32, hipMemcpyHostToDevice, d.stream));
+  if (bytes) HIP_OK(hipMemcpyAsync(d.blob.p, msg_blob + b0, bytes, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.stream));
+  HIP_OK(hipMemcpyAsync(d.off.p, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(pv::launch_sign(d.tamper.p, d.blob.p, d.off.p, n, d.btab.p, d.pk.p, d.sig.p, d.stream));
+  HIP_OK(hipMemcpyAsync(pk_out, d.pk.p, n * 32, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipMemcpyAsync(sig_out, d.sig.p, n * 64, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipStreamSynchronize(d.stream));
+  return PV_OK;
+}
+
+int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen, uint64_t* off,
+                    uint8_t* blob, uint8_t* seeds, uint8_t* pk, uint8_t* sig, uint8_t* tamper, int device,
+                    void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (!off || !blob || !seeds || !pk || !sig || !tamper) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(pv::launch_synth(cfg, first, n, key_mod, mlen, 0, 0, off, seeds, tamper, s));
+  HIP_OK(pv::launch_synth_fill(cfg, first, n, off, blob, s));
+  HIP_OK(hipMemsetAsync(blob + n * (uint64_t)mlen, 0, 16, s));
+  HIP_OK(pv::launch_sign(seeds, blob, off, n, d->btab.p, pk, sig, s));
+  HIP_OK(pv::launch_tamper(first, n, tamper, off, blob, sig, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+}  // extern "C"

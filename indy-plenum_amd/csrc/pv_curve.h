@@ -1,0 +1,214 @@
+// Edwards25519 group operations for the batch verifier (twisted Edwards,
+// a = -1, extended coordinates).  Complete unified formulas, so the identity
+// and torsion points need no special cases: that is what lets every lane of a
+// wavefront run the SAME fixed-window schedule (no data-dependent branches).
+//
+// Point forms (as in the libsodium/ref10 family the reference binds):
+//   p2     (X:Y:Z)                       x = X/Z, y = Y/Z
+//   p3     (X:Y:Z:T)                     T = XY/Z
+//   p1p1   completed ((X:Z),(Y:T))       x = X/Z, y = Y/T
+//   cached (Y+X, Y-X, 2Z, 2dT)           projective table entry ("2Z" keeps
+//                                        the add's D term TIGHT)
+//   niels  (y+x, y-x, 2dxy)              affine table entry (base-point table)
+#pragma once
+#include "pv_field.h"
+
+namespace pv {
+
+struct ge_p2 { fe X, Y, Z; };
+struct ge_p3 { fe X, Y, Z, T; };
+struct ge_p1p1 { fe X, Y, Z, T; };
+struct ge_cached { fe YpX, YmX, Z2, T2d; };
+struct ge_niels { fe ypx, ymx, xy2d; };
+
+PV_HD void ge_p3_0(ge_p3& h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); fe_0(h.T); }
+
+PV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+}
+
+PV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+}
+
+// dbl-2008-hwcd (a = -1) from p2:  r.X = 2XY, r.Y = Y^2+X^2, r.Z = Y^2-X^2, r.T = 2Z^2-(Y^2-X^2)
+PV_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
+  fe xx, yy, zz2, xy2, t;
+  fe_sq(xx, p.X);
+  fe_sq(yy, p.Y);
+  fe_sq(zz2, p.Z);
+  fe_add(t, p.X, p.Y);         // LOOSE
+  fe_sq(xy2, t);               // (X+Y)^2
+  fe_add(r.Y, yy, xx);         // LOOSE
+  fe_sub(r.Z, yy, xx);         // LOOSE
+  fe_sub4(r.X, xy2, r.Y);      // (X+Y)^2 - X^2 - Y^2 = 2XY
+  fe_carry(r.X);
+  fe_add(t, zz2, zz2);         // 2Z^2, even limbs <= 2^27
+  fe_sub4(r.T, t, r.Z);
+  fe_carry(r.T);
+}
+
+PV_HD void ge_p3_dbl(ge_p1p1& r, const ge_p3& p) {
+  ge_p2 q;
+  fe_copy(q.X, p.X);
+  fe_copy(q.Y, p.Y);
+  fe_copy(q.Z, p.Z);
+  ge_p2_dbl(r, q);
+}
+
+PV_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
+  fe d2;
+  fe_const_d2(d2);
+  fe_add(r.YpX, p.Y, p.X);
+  fe_sub(r.YmX, p.Y, p.X);
+  fe_add(r.Z2, p.Z, p.Z);
+  fe_mul(r.T2d, p.T, d2);
+}
+
+PV_HD void ge_cached_identity(ge_cached& r) {
+  fe_1(r.YpX);
+  fe_1(r.YmX);
+  fe_0(r.Z2);
+  r.Z2.v[0] = 2;
+  fe_0(r.T2d);
+}
+
+// r = p + s*q   (s = sign: false add, true subtract), q cached.  Branch-free.
+PV_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q, bool neg) {
+  fe ypx1, ymx1, a, b, c, d, qa, qb;
+  fe_add(ypx1, p.Y, p.X);
+  fe_sub(ymx1, p.Y, p.X);
+  fe_cmov(qa, q.YpX, q.YmX, neg);
+  fe_cmov(qb, q.YmX, q.YpX, neg);
+  fe_mul(a, ypx1, qa);
+  fe_mul(b, ymx1, qb);
+  fe_mul(c, q.T2d, p.T);
+  fe_mul(d, p.Z, q.Z2);        // TIGHT 2*Z1*Z2
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe e, f;
+  fe_add(e, d, c);
+  fe_sub(f, d, c);
+  fe_cmov(r.Z, e, f, neg);
+  fe_cmov(r.T, f, e, neg);
+}
+
+// r = p + s*q, q affine niels (base-point table)
+PV_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q, bool neg) {
+  fe ypx1, ymx1, a, b, c, d, qa, qb;
+  fe_add(ypx1, p.Y, p.X);
+  fe_sub(ymx1, p.Y, p.X);
+  fe_cmov(qa, q.ypx, q.ymx, neg);
+  fe_cmov(qb, q.ymx, q.ypx, neg);
+  fe_mul(a, ypx1, qa);
+  fe_mul(b, ymx1, qb);
+  fe_mul(c, q.xy2d, p.T);
+  fe_add(d, p.Z, p.Z);
+  fe_carry(d);                 // TIGHT so that d - c stays LOOSE
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe e, f;
+  fe_add(e, d, c);
+  fe_sub(f, d, c);
+  fe_cmov(r.Z, e, f, neg);
+  fe_cmov(r.T, f, e, neg);
+}
+
+// Decompress s and NEGATE (returns -P, x chosen with parity != sign bit).
+// Restates ge25519_frombytes_negate_vartime's contract (SURVEY.md App. C.2
+// step 4): fails iff (y^2-1)/(dy^2+1) has no square root; x == 0 with the
+// sign bit set is accepted (libsodium 1.0.18).
+PV_HD bool ge_frombytes_negate(ge_p3& h, const uint32_t s[8]) {
+  fe u, v, v3, vxx, chk, one, d;
+  fe_const_d(d);
+  fe_1(one);
+  fe_frombytes_w(h.Y, s);
+  fe_1(h.Z);
+  fe_sq(u, h.Y);
+  fe_mul(v, u, d);
+  fe_sub(u, u, one);
+  fe_carry(u);                 // y^2 - 1, TIGHT
+  fe_add(v, v, one);           // d y^2 + 1, LOOSE
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);           // v^3
+  fe_sq(h.X, v3);
+  fe_mul(h.X, h.X, v);
+  fe_mul(h.X, h.X, u);         // u v^7
+  fe_pow22523(h.X, h.X);
+  fe_mul(h.X, h.X, v3);
+  fe_mul(h.X, h.X, u);         // u v^3 (u v^7)^((p-5)/8)
+  fe_sq(vxx, h.X);
+  fe_mul(vxx, vxx, v);
+  fe_sub(chk, vxx, u);
+  bool ok = true;
+  if (!fe_iszero(chk)) {
+    fe_add(chk, vxx, u);
+    if (!fe_iszero(chk)) ok = false;
+    fe sqrtm1;
+    fe_const_sqrtm1(sqrtm1);
+    fe_mul(h.X, h.X, sqrtm1);
+  }
+  const uint32_t sign = s[7] >> 31;
+  fe nx;
+  fe_neg(nx, h.X);
+  fe_carry(nx);
+  fe_cmov(h.X, h.X, nx, fe_isnegative(h.X) == sign);
+  fe_mul(h.T, h.X, h.Y);
+  return ok;
+}
+
+// canonical encoding of a p2 point as 8 LE words (y | sign(x) << 255)
+PV_HD void ge_p2_tobytes(uint32_t w[8], const ge_p2& p) {
+  fe zi, x, y;
+  fe_invert(zi, p.Z);
+  fe_mul(x, p.X, zi);
+  fe_mul(y, p.Y, zi);
+  fe_tobytes_w(w, y);
+  w[7] ^= fe_isnegative(x) << 31;
+}
+
+PV_HD void ge_p3_tobytes(uint32_t w[8], const ge_p3& p) {
+  ge_p2 q;
+  fe_copy(q.X, p.X);
+  fe_copy(q.Y, p.Y);
+  fe_copy(q.Z, p.Z);
+  ge_p2_tobytes(w, q);
+}
+
+// small-order encodings refused by libsodium 1.0.18,
+// compared with bit 255 cleared
+PV_HD bool has_small_order(const uint32_t s[8]) {
+  const uint32_t bl[7][8] = {
+      {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u},
+      {1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u},
+      {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
+      {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
+      {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+      {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+      {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+  };
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) diff |= s[i] ^ bl[k][i];
+    diff |= (s[7] & 0x7fffffffu) ^ bl[k][7];
+    any = any || diff == 0;
+  }
+  return any;
+}
+
+// y (bit 255 cleared) < p  (ge25519_is_canonical, App. C.2 step 3)
+PV_HD bool y_is_canonical(const uint32_t s[8]) {
+  uint32_t all1 = s[1] & s[2] & s[3] & s[4] & s[5] & s[6];
+  const bool top = (s[7] & 0x7fffffffu) == 0x7fffffffu && all1 == 0xffffffffu;
+  return !(top && s[0] >= 0xffffffedu);
+}
+
+}  // namespace pv

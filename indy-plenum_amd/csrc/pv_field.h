@@ -1,0 +1,326 @@
+// GF(2^255 - 19) arithmetic for the batch verifier, one field element per lane.
+//
+// Representation: 10 unsigned 32-bit limbs in radix 2^25.5 (limb i has weight
+// 2^ceil(25.5 i): 0,26,51,77,102,128,153,179,204,230).  Products are formed
+// with v_mad_u64_u32 (32x32 -> 64-bit multiply-accumulate), which measures
+// ~45 lane-ops/clk/CU on gfx950 (profiles/r01_int_rates.json) and is the
+// instruction the roofline is priced in.  MFMA is not used: this is modular
+// 255-bit arithmetic, not a dense contraction.
+//
+// Bound discipline (checked by the host bound-checking build, tests/test_host_arith.py):
+//   TIGHT  : even limbs <= 2^26 + 2^10, odd limbs <= 2^25 + 2^17   (mul/sq/carry output)
+//   LOOSE  : even limbs <= 2^27.7,      odd limbs <= 2^26.7        (mul/sq input limit)
+//   tight+tight, tight+tight+tight and tight + 2p - tight are LOOSE.
+//
+// Restates the field layer libsodium 1.0.18 uses under crypto_sign_open
+// (SURVEY.md Appendix C); the verdict only depends on exact field results, so
+// any exact representation is parity-equivalent.
+#pragma once
+#include <stdint.h>
+
+#ifndef PV_HD
+#define PV_HD __host__ __device__ __forceinline__
+#endif
+#ifndef PV_COUNT
+#define PV_COUNT(kind)
+#endif
+#ifndef PV_CHECK_LOOSE
+#define PV_CHECK_LOOSE(f)
+#endif
+
+namespace pv {
+
+static constexpr uint32_t M26 = (1u << 26) - 1;
+static constexpr uint32_t M25 = (1u << 25) - 1;
+
+struct fe {
+  uint32_t v[10];
+};
+
+PV_HD uint64_t mul32x32(uint32_t a, uint32_t b) { return (uint64_t)a * (uint64_t)b; }
+
+PV_HD void fe_0(fe& h) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = 0;
+}
+PV_HD void fe_1(fe& h) {
+  fe_0(h);
+  h.v[0] = 1;
+}
+PV_HD void fe_copy(fe& h, const fe& f) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = f.v[i];
+}
+
+// 64-bit column sums -> TIGHT limbs.  Two interleaved carry chains (0..4 and
+// 4..9) keep the dependency depth short; final wrap multiplies by 19 because
+// 2^255 == 19 (mod p).
+PV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
+  uint64_t c;
+  c = h[0] >> 26; h[1] += c; h[0] &= M26;
+  c = h[4] >> 26; h[5] += c; h[4] &= M26;
+  c = h[1] >> 25; h[2] += c; h[1] &= M25;
+  c = h[5] >> 25; h[6] += c; h[5] &= M25;
+  c = h[2] >> 26; h[3] += c; h[2] &= M26;
+  c = h[6] >> 26; h[7] += c; h[6] &= M26;
+  c = h[3] >> 25; h[4] += c; h[3] &= M25;
+  c = h[7] >> 25; h[8] += c; h[7] &= M25;
+  c = h[4] >> 26; h[5] += c; h[4] &= M26;
+  c = h[8] >> 26; h[9] += c; h[8] &= M26;
+  c = h[9] >> 25; h[0] += c * 19; h[9] &= M25;
+  c = h[0] >> 26; h[1] += c; h[0] &= M26;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) out.v[i] = (uint32_t)h[i];
+}
+
+// h = f * g.  Column k collects f_i g_j with i + j = k (weight doubles when i
+// and j are both odd) and, wrapped, 19 f_i g_j with i + j = k + 10.
+PV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+  PV_COUNT(mul);
+  PV_CHECK_LOOSE(f);
+  PV_CHECK_LOOSE(g);
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int j = 1; j < 10; ++j) g19[j] = 19u * g.v[j];
+#pragma unroll
+  for (int i = 1; i < 10; i += 2) f2[i] = 2u * f.v[i];
+  uint64_t acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const bool oo = (i & 1) && (j & 1);
+      const uint32_t a = oo ? f2[i] : f.v[i];
+      const int k = i + j;
+      if (k < 10) acc[k] += mul32x32(a, g.v[j]);
+      else acc[k - 10] += mul32x32(a, g19[j]);
+    }
+  }
+  fe_carry_wide(h, acc);
+}
+
+// h = f^2 with the symmetric cross terms folded (55 products instead of 100).
+PV_HD void fe_sq(fe& h, const fe& f) {
+  PV_COUNT(sq);
+  PV_CHECK_LOOSE(f);
+  uint32_t f2[10], f19[10], f4[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) f2[i] = 2u * f.v[i];
+#pragma unroll
+  for (int i = 5; i < 10; ++i) f19[i] = 19u * f.v[i];
+#pragma unroll
+  for (int i = 1; i < 10; i += 2) f4[i] = 4u * f.v[i];
+  uint64_t acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int j = i; j < 10; ++j) {
+      const bool oo = (i & 1) && (j & 1);
+      const int k = i + j;
+      uint32_t a, b;
+      if (i == j) {
+        // f_i^2 (x2 if odd) (x19 if wrapped)
+        if (k < 10) { a = f.v[i]; b = oo ? f2[i] : f.v[i]; }
+        else { a = oo ? f2[i] : f.v[i]; b = f19[i]; }
+      } else {
+        // 2 f_i f_j (x2 if both odd) (x19 if wrapped)
+        if (k < 10) { a = oo ? f4[i] : f2[i]; b = f.v[j]; }
+        else { a = oo ? f4[i] : f2[i]; b = f19[j]; }
+      }
+      if (k < 10) acc[k] += mul32x32(a, b);
+      else acc[k - 10] += mul32x32(a, b);
+    }
+  }
+  fe_carry_wide(h, acc);
+}
+
+PV_HD void fe_sqn(fe& h, const fe& f, int n) {
+  fe_sq(h, f);
+  for (int i = 1; i < n; ++i) fe_sq(h, h);
+}
+
+PV_HD void fe_add(fe& h, const fe& f, const fe& g) {
+  PV_COUNT(add);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + g.v[i];
+}
+
+// 2p in radix 2^25.5
+static constexpr uint32_t P2_0 = 2u * ((1u << 26) - 19);
+static constexpr uint32_t P2_E = 2u * ((1u << 26) - 1);
+static constexpr uint32_t P2_O = 2u * ((1u << 25) - 1);
+
+// h = f - g + 2p ; g must be TIGHT.  LOOSE result when f is TIGHT.
+PV_HD void fe_sub(fe& h, const fe& f, const fe& g) {
+  PV_COUNT(add);
+  h.v[0] = f.v[0] + P2_0 - g.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; ++i) h.v[i] = f.v[i] + ((i & 1) ? P2_O : P2_E) - g.v[i];
+}
+
+// h = f - g + 4p ; g may be LOOSE up to 2^28 / 2^27.  Result needs fe_carry.
+PV_HD void fe_sub4(fe& h, const fe& f, const fe& g) {
+  PV_COUNT(add);
+  h.v[0] = f.v[0] + 2u * P2_0 - g.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; ++i) h.v[i] = f.v[i] + 2u * ((i & 1) ? P2_O : P2_E) - g.v[i];
+}
+
+// -f = 2p - f (f TIGHT) -> LOOSE
+PV_HD void fe_neg(fe& h, const fe& f) {
+  PV_COUNT(add);
+  h.v[0] = P2_0 - f.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; ++i) h.v[i] = ((i & 1) ? P2_O : P2_E) - f.v[i];
+}
+
+// one carry pass over 32-bit limbs (inputs up to ~2^31): -> TIGHT
+PV_HD void fe_carry(fe& h) {
+  PV_COUNT(carry);
+  uint32_t c;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+  c = h.v[1] >> 25; h.v[1] &= M25; h.v[2] += c;
+  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
+  c = h.v[3] >> 25; h.v[3] &= M25; h.v[4] += c;
+  c = h.v[4] >> 26; h.v[4] &= M26; h.v[5] += c;
+  c = h.v[5] >> 25; h.v[5] &= M25; h.v[6] += c;
+  c = h.v[6] >> 26; h.v[6] &= M26; h.v[7] += c;
+  c = h.v[7] >> 25; h.v[7] &= M25; h.v[8] += c;
+  c = h.v[8] >> 26; h.v[8] &= M26; h.v[9] += c;
+  c = h.v[9] >> 25; h.v[9] &= M25; h.v[0] += 19u * c;
+}
+
+// conditional select: h = c ? g : f  (lane-local, branch-free)
+PV_HD void fe_cmov(fe& h, const fe& f, const fe& g, bool c) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = c ? g.v[i] : f.v[i];
+}
+
+// 32-byte little-endian (as 8 words) -> limbs; bit 255 dropped (value < 2^255, TIGHT)
+PV_HD void fe_frombytes_w(fe& h, const uint32_t w[8]) {
+  h.v[0] = w[0] & M26;
+  h.v[1] = ((w[0] >> 26) | (w[1] << 6)) & M25;
+  h.v[2] = ((w[1] >> 19) | (w[2] << 13)) & M26;
+  h.v[3] = ((w[2] >> 13) | (w[3] << 19)) & M25;
+  h.v[4] = (w[3] >> 6) & M26;
+  h.v[5] = w[4] & M25;
+  h.v[6] = ((w[4] >> 25) | (w[5] << 7)) & M26;
+  h.v[7] = ((w[5] >> 19) | (w[6] << 13)) & M25;
+  h.v[8] = ((w[6] >> 12) | (w[7] << 20)) & M26;
+  h.v[9] = (w[7] >> 6) & M25;
+}
+
+// canonical (fully reduced mod p) little-endian words.  Accepts any limbs a
+// single fe_carry pass brings to TIGHT (value then < 2p).
+PV_HD void fe_tobytes_w(uint32_t w[8], const fe& f) {
+  fe h;
+  fe_copy(h, f);
+  fe_carry(h);
+  fe_carry(h);
+  // q = [h >= p] = carry out of h + 19 at bit 255
+  uint32_t q = (h.v[0] + 19u) >> 26;
+  q = (h.v[1] + q) >> 25;
+  q = (h.v[2] + q) >> 26;
+  q = (h.v[3] + q) >> 25;
+  q = (h.v[4] + q) >> 26;
+  q = (h.v[5] + q) >> 25;
+  q = (h.v[6] + q) >> 26;
+  q = (h.v[7] + q) >> 25;
+  q = (h.v[8] + q) >> 26;
+  q = (h.v[9] + q) >> 25;
+  h.v[0] += 19u * q;
+  uint32_t c;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+  c = h.v[1] >> 25; h.v[1] &= M25; h.v[2] += c;
+  c = h.v[2] >> 26; h.v[2] &= M26; h.v[3] += c;
+  c = h.v[3] >> 25; h.v[3] &= M25; h.v[4] += c;
+  c = h.v[4] >> 26; h.v[4] &= M26; h.v[5] += c;
+  c = h.v[5] >> 25; h.v[5] &= M25; h.v[6] += c;
+  c = h.v[6] >> 26; h.v[6] &= M26; h.v[7] += c;
+  c = h.v[7] >> 25; h.v[7] &= M25; h.v[8] += c;
+  c = h.v[8] >> 26; h.v[8] &= M26; h.v[9] += c;
+  h.v[9] &= M25;  // the dropped carry is q * 2^255
+  w[0] = h.v[0] | (h.v[1] << 26);
+  w[1] = (h.v[1] >> 6) | (h.v[2] << 19);
+  w[2] = (h.v[2] >> 13) | (h.v[3] << 13);
+  w[3] = (h.v[3] >> 19) | (h.v[4] << 6);
+  w[4] = h.v[5] | (h.v[6] << 25);
+  w[5] = (h.v[6] >> 7) | (h.v[7] << 19);
+  w[6] = (h.v[7] >> 13) | (h.v[8] << 12);
+  w[7] = (h.v[8] >> 20) | (h.v[9] << 6);
+}
+
+PV_HD bool fe_iszero(const fe& f) {
+  uint32_t w[8];
+  fe_tobytes_w(w, f);
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d |= w[i];
+  return d == 0;
+}
+
+PV_HD uint32_t fe_isnegative(const fe& f) {
+  uint32_t w[8];
+  fe_tobytes_w(w, f);
+  return w[0] & 1u;
+}
+
+// z^(2^250 - 1) and z^11, the common prefix of the inversion and sqrt chains
+PV_HD void fe_pow_2_250_1(fe& out, fe& z11, const fe& z) {
+  fe z2, z9, t, a, b, c;
+  fe_sq(z2, z);
+  fe_sqn(t, z2, 2);
+  fe_mul(z9, t, z);
+  fe_mul(z11, z9, z2);
+  fe_sq(t, z11);
+  fe_mul(a, t, z9);                    // 2^5 - 1
+  fe_sqn(t, a, 5);    fe_mul(b, t, a); // 2^10 - 1
+  fe_sqn(t, b, 10);   fe_mul(c, t, b); // 2^20 - 1
+  fe_sqn(t, c, 20);   fe_mul(t, t, c); // 2^40 - 1
+  fe_sqn(t, t, 10);   fe_mul(a, t, b); // 2^50 - 1
+  fe_sqn(t, a, 50);   fe_mul(b, t, a); // 2^100 - 1
+  fe_sqn(t, b, 100);  fe_mul(t, t, b); // 2^200 - 1
+  fe_sqn(t, t, 50);   fe_mul(out, t, a); // 2^250 - 1
+}
+
+// z^(p-2)
+PV_HD void fe_invert(fe& h, const fe& z) {
+  fe t, z11;
+  fe_pow_2_250_1(t, z11, z);
+  fe_sqn(t, t, 5);
+  fe_mul(h, t, z11);
+}
+
+// z^((p-5)/8)
+PV_HD void fe_pow22523(fe& h, const fe& z) {
+  fe t, z11;
+  fe_pow_2_250_1(t, z11, z);
+  fe_sqn(t, t, 2);
+  fe_mul(h, t, z);
+}
+
+// curve constants as TIGHT limbs (values checked against the oracle in tests)
+PV_HD void fe_const_d(fe& h) {  // d = -121665/121666
+  const uint32_t v[10] = {56195235u, 13857412u, 51736253u, 6949390u, 114729u,
+                          24766616u, 60832955u, 30306712u, 48412415u, 21499315u};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = v[i];
+}
+PV_HD void fe_const_d2(fe& h) {  // 2d
+  const uint32_t v[10] = {45281625u, 27714825u, 36363642u, 13898781u, 229458u,
+                          15978800u, 54557047u, 27058993u, 29715967u, 9444199u};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = v[i];
+}
+PV_HD void fe_const_sqrtm1(fe& h) {  // 2^((p-1)/4)
+  const uint32_t v[10] = {34513072u, 25610706u, 9377949u, 3500415u, 12389472u,
+                          33281959u, 41962654u, 31548777u, 326685u, 11406482u};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = v[i];
+}
+
+}  // namespace pv

@@ -1,0 +1,56 @@
+// Internal launch interface between the C-ABI layer (pv_api.cpp) and the HIP
+// kernels (pv_kernels.hip).  All pointers are device pointers on the current
+// device; every launch is asynchronous on `stream`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pv {
+
+// base-point table: 129 niels entries (k*B, k = 0..128), 32 words each
+constexpr int BTAB_ENTRIES = 129;
+constexpr int BTAB_WORDS = 32;
+// per-lane A table: 9 cached entries (k*(-A), k = 0..8), 40 words each
+constexpr int ATAB_WORDS = 9 * 40;
+constexpr int CURVE_BLOCK = 256;
+constexpr int HASH_BLOCK = 256;
+
+struct DeviceCaps {
+  int cu_count;
+  int curve_blocks;  // persistent grid for the curve kernel
+};
+
+hipError_t launch_btable_init(uint32_t* btab, hipStream_t s);
+
+// resident curve-kernel blocks per CU (occupancy query)
+hipError_t curve_occupancy(int* blocks_per_cu);
+
+// pre[i] = 1 iff S canonical, R/A not small order, A canonical;
+// h[i] (8 words) = SHA-512(R||A||M) mod L
+hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                       uint64_t n, uint32_t* h, uint8_t* pre, hipStream_t s);
+
+// verdict[i] in {0,1}; bitmap[i/64] bit i%64 (bitmap must hold ceil(n/64) words)
+hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
+                        const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
+                        uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s);
+
+// keygen + sign: pk[i], sig[i] for seed[i] over M_i
+hipError_t launch_sign(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n,
+                       const uint32_t* btab, uint8_t* pk_out, uint8_t* sig_out, hipStream_t s);
+
+// per-batch quorum tally over verdicts
+hipError_t launch_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off,
+                        uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t* votes,
+                        uint8_t* reached, hipStream_t s);
+
+// deterministic synthetic workload; see plenum_gpu/synth.py
+hipError_t launch_synth(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen_fixed,
+                        uint32_t mlen_min, uint32_t mlen_max, uint64_t* off_out, uint8_t* seeds_out,
+                        uint8_t* tamper_out, hipStream_t s);
+hipError_t launch_synth_fill(uint32_t cfg, uint64_t first, uint64_t n, const uint64_t* off, uint8_t* blob,
+                             hipStream_t s);
+hipError_t launch_tamper(uint64_t first, uint64_t n, const uint8_t* tamper, const uint64_t* off, uint8_t* blob,
+                         uint8_t* sig, hipStream_t s);
+
+}  // namespace pv

@@ -1,0 +1,154 @@
+"""ctypes binding of libplenum_verify.so (include/plenum_verify.h).
+
+This is the ONLY way the package reaches the verifier: there is no CPU
+fallback.  If the shared library is missing, or no GPU is present when a
+compute entry point is called, the call raises — loudly — instead of silently
+verifying on the host.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('PLENUM_GPU_LIB', os.path.join(os.path.dirname(_HERE), 'lib', 'libplenum_verify.so'))
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+
+# (name, restype, argtypes) exactly as declared in include/plenum_verify.h
+SIGNATURES = [
+    ('pv_init', ctypes.c_int, [ctypes.c_uint32]),
+    ('pv_shutdown', None, []),
+    ('pv_last_error', ctypes.c_char_p, []),
+    ('pv_device_count', ctypes.c_int, []),
+    ('pv_verify_batch', ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, ctypes.c_uint32]),
+    ('pv_verify_batch_device', ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_tally', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ('pv_tally_device', ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_sign_batch', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    ('pv_sign_batch_device', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_synth_device', ctypes.c_int,
+     [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp,
+      _vp, ctypes.c_int, _vp]),
+    ('pv_time_verify_device', ctypes.c_int,
+     [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int,
+      ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+]
+
+
+class PlenumGpuError(RuntimeError):
+    """A C-ABI call returned a negative code (message from pv_last_error)."""
+
+    def __init__(self, fn, code, msg):
+        super().__init__('{} failed ({}): {}'.format(fn, code, msg))
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+_inited = False
+
+
+def load():
+    """Load the shared library (raises OSError if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError('libplenum_verify.so not found at {} — build it with '
+                          '`python indy-plenum_amd/build.py` (there is no CPU fallback)'.format(LIB_PATH))
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _check(fn, rc):
+    if rc != 0:
+        raise PlenumGpuError(fn, rc, load().pv_last_error().decode(errors='replace'))
+
+
+def ensure_init(device_mask=0):
+    """pv_init once per process; raises PlenumGpuError when no GPU is usable."""
+    global _inited
+    with _lock:
+        if not _inited:
+            _check('pv_init', load().pv_init(device_mask))
+            _inited = True
+
+
+def shutdown():
+    global _inited
+    with _lock:
+        if _lib is not None:
+            _lib.pv_shutdown()
+        _inited = False
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else ctypes.c_void_p(0)
+
+
+def pack_messages(msgs):
+    """list[bytes] -> (blob uint8, off uint64[n+1])."""
+    n = len(msgs)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    if n:
+        off[1:] = np.cumsum(np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=n))
+    blob = np.frombuffer(b''.join(msgs), dtype=np.uint8) if n else np.zeros(0, np.uint8)
+    return blob, off
+
+
+def verify_batch_arrays(pk, sig, blob, off, device_mask=0):
+    """pk (n,32) u8, sig (n,64) u8, blob u8, off (n+1) u64 -> verdict (n,) bool."""
+    ensure_init()
+    pk = np.ascontiguousarray(pk, dtype=np.uint8)
+    sig = np.ascontiguousarray(sig, dtype=np.uint8)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    n = pk.shape[0]
+    if sig.shape[0] != n or off.shape[0] != n + 1 or (n and pk.shape[1] != 32) or (n and sig.shape[1] != 64):
+        raise ValueError('shape mismatch: pk {}, sig {}, off {}'.format(pk.shape, sig.shape, off.shape))
+    if n and int(off[-1]) > blob.size:
+        raise ValueError('msg_off exceeds blob size')
+    verdict = np.zeros(n, dtype=np.uint8)
+    if n == 0:
+        return verdict.astype(bool)
+    _check('pv_verify_batch', load().pv_verify_batch(_ptr(pk), _ptr(sig), _ptr(blob), _ptr(off), n, _ptr(verdict),
+                                                      device_mask, 0))
+    return verdict.astype(bool)
+
+
+def tally_arrays(verdict, sender, batch_off, n_nodes, quorum):
+    ensure_init()
+    verdict = np.ascontiguousarray(verdict, dtype=np.uint8)
+    sender = np.ascontiguousarray(sender, dtype=np.uint32)
+    batch_off = np.ascontiguousarray(batch_off, dtype=np.uint64)
+    nb = batch_off.shape[0] - 1
+    votes = np.zeros(max(nb, 0), dtype=np.uint32)
+    reached = np.zeros(max(nb, 0), dtype=np.uint8)
+    if nb <= 0:
+        return votes, reached.astype(bool)
+    _check('pv_tally', load().pv_tally(_ptr(verdict), _ptr(sender), _ptr(batch_off), nb, n_nodes, quorum,
+                                        _ptr(votes), _ptr(reached)))
+    return votes, reached.astype(bool)
+
+
+def sign_batch_arrays(seeds, blob, off):
+    ensure_init()
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    n = seeds.shape[0]
+    pk = np.zeros((n, 32), dtype=np.uint8)
+    sig = np.zeros((n, 64), dtype=np.uint8)
+    if n:
+        _check('pv_sign_batch', load().pv_sign_batch(_ptr(seeds), _ptr(blob), _ptr(off), n, _ptr(pk), _ptr(sig)))
+    return pk, sig
