@@ -1,0 +1,214 @@
+"""Bench: Ed25519 verifies/s on MI355X (BASELINE.json metric, config C2).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one pass of the hot path (hash kernel + curve kernel: libsodium-
+exact Ed25519 verification) over one rank's batch of 1,000,000 synthetic
+signed requests (distinct keys, 256 B payloads, ~5 % tampered) that is already
+resident in HBM, plus — when N > 1 — the RCCL all-gather of every rank's
+packed verdict bitmap.  Weak scaling: each rank owns a disjoint index range.
+
+Rank 0 prints ONE JSON line.  `value` = all ranks' verifies / max-over-ranks
+time.  `roofline` prices the dominant (curve) kernel against the measured
+v_mad_u64_u32 issue rate; `cpu_baseline` times libsodium 1.0.18 (the native
+call under Plenum's Verifier.verify) on the host cores, rank 0, N = 1 only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'indy-plenum_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from plenum_gpu import _native as nat  # noqa: E402
+from plenum_gpu.device import SyntheticBatch  # noqa: E402
+
+METRIC = 'Ed25519 verifies/sec at 1/2/4/8 MI355X vs libsodium on host cores'
+N_PER_RANK = 1_000_000
+MLEN = 256
+CFG = 2
+
+# Algorithmic work of the curve kernel per verify, counted by the host
+# instrumentation build of the same code (tests/test_hostcheck.py pins these):
+# field multiplies x 100 + squarings x 55 v_mad_u64_u32 (radix 2^25.5 schoolbook).
+W_MUL_PER_VERIFY = 1588
+W_SQ_PER_VERIFY = 1517
+W_MAD_PER_VERIFY = W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55
+# v_mad_u64_u32 issue rate of one MI355X measured by tools/ubench/int_rates.hip
+# (profiles/r01_int_rates.json): lane-ops/s over the whole chip.
+P_MAD_PER_S = 2.7875e13
+
+
+def _mad_peak():
+    path = os.path.join(REPO, 'profiles', 'r01_int_rates.json')
+    try:
+        with open(path) as fh:
+            for r in json.load(fh)['results']:
+                if r['insn'] == 'v_mad_u64_u32':
+                    return float(r['lane_ops_per_s'])
+    except (OSError, KeyError, ValueError):
+        pass
+    return P_MAD_PER_S
+
+
+def _traffic_per_launch():
+    """HBM bytes per curve launch from the committed rocprofv3 PMC summary, or None."""
+    path = os.path.join(REPO, 'profiles', 'r01_curve_pmc.json')
+    try:
+        with open(path) as fh:
+            return json.load(fh).get('hbm_bytes_per_launch')
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(batch, seconds=1.5, sample=8192):
+    """libsodium crypto_sign_verify_detached on the host cores over the first
+    `sample` signatures of this rank's workload (copied to host)."""
+    so = os.path.join(REPO, 'oracle', 'liboracle.so')
+    if not os.path.exists(so):
+        return None
+    lib = ctypes.CDLL(so)
+    lib.cpu_baseline_rate.restype = ctypes.c_double
+    lib.cpu_baseline_rate.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_double,
+                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64)]
+    pk = batch.pk[:sample].cpu().numpy().copy()
+    sig = batch.sig[:sample].cpu().numpy().copy()
+    off = batch.off[:sample + 1].cpu().numpy().astype(np.uint64)
+    blob = batch.blob[:int(off[-1]) + 16].cpu().numpy().copy()
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get('OMP_NUM_THREADS', threads)))
+    kind = ctypes.c_int()
+    acc = ctypes.c_uint64()
+    p = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    sodium = b'/opt/conda/lib/libsodium.so.23'
+    rate = lib.cpu_baseline_rate(sodium, p(pk), p(sig), p(blob), p(off), sample, threads, seconds,
+                                 ctypes.byref(kind), ctypes.byref(acc))
+    rate1 = lib.cpu_baseline_rate(sodium, p(pk), p(sig), p(blob), p(off), sample, 1, min(seconds, 1.0),
+                                  ctypes.byref(kind), ctypes.byref(acc))
+    cpu = ''
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    cpu = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    name = 'libsodium 1.0.18 crypto_sign_verify_detached' if kind.value == 0 else \
+        'C restatement oracle/ed25519_oracle.c (libsodium not loadable)'
+    return {'value': round(rate, 1), 'unit': 'verifies/s', 'cores': threads,
+            'kind': 'reference' if kind.value == 0 else 'port',
+            'sample': '{} ({} threads, {:.1f} s wall; 1 thread: {:.1f} verifies/s) over the first {} signatures '
+                      'of the C2 workload, host {}'.format(name, threads, seconds, rate1, sample, cpu)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--n', type=int, default=N_PER_RANK, help='signatures per GPU (default: C2, 1M)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    n = args.n
+    batch = SyntheticBatch(local, n, MLEN, cfg=CFG, first=rank * n)
+    torch.cuda.synchronize()
+    gathered = torch.zeros(world * batch.bitmap.numel(), dtype=torch.int64, device=dev) if world > 1 else None
+
+    def step():
+        batch.verify()
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, batch.bitmap)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness of the measured pass: verdict == not tampered, bitmap == verdict
+    verdict = batch.verdict.cpu().numpy().astype(bool)
+    tamper = batch.tamper.cpu().numpy().astype(bool)
+    mism = int((verdict == tamper).sum())
+    bits = np.unpackbits(batch.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
+    mism += int((bits != verdict).sum())
+    if world > 1:
+        allbits = np.unpackbits(gathered.cpu().numpy().view(np.uint8), bitorder='little')
+        per = batch.bitmap.numel() * 64
+        mine = allbits[rank * per: rank * per + n].astype(bool)
+        mism += int((mine != verdict).sum())
+        m = torch.tensor([mism], dtype=torch.int64, device=dev)
+        dist.all_reduce(m)
+        mism = int(m.item())
+
+    # kernel-level timing (HIP events on the launch stream) for the roofline
+    ms_hash, ms_curve = batch.time_kernels(3)
+    achieved = W_MAD_PER_VERIFY * n / (ms_curve * 1e-3)
+    peak = _mad_peak()
+
+    total = world * n * args.steps
+    value = total / elapsed
+    out = {
+        'metric': METRIC, 'value': round(value, 1), 'unit': 'verifies/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',
+        'data': 'synthetic (device-generated, deterministic: plenum_gpu/synth.py)',
+        'config': {'workload': 'C2: 1M Ed25519 request signatures per GPU, distinct keys, 256 B payloads, '
+                               '~5% tampered (BASELINE.json configs[1])',
+                   'signatures_per_gpu': n, 'msg_bytes': MLEN, 'tampered': int(tamper.sum()),
+                   'parallelism': 'dp{} (disjoint index shards) + RCCL all-gather of verdict bitmaps'.format(world)
+                   if world > 1 else 'single GPU'},
+        'verdict_mismatches': mism,
+        'kernel_ms': {'hash': round(ms_hash, 4), 'curve': round(ms_curve, 4)},
+        'roofline': {'bound': 'valu', 'kernel': 'k_curve',
+                     'achieved': round(achieved / 1e12, 3), 'peak': round(peak / 1e12, 3),
+                     'unit': 'Tmad/s (v_mad_u64_u32 lane-ops)', 'frac': round(achieved / peak, 4),
+                     'traffic': _traffic_per_launch(),
+                     'work_per_verify': {'fe_mul': W_MUL_PER_VERIFY, 'fe_sq': W_SQ_PER_VERIFY,
+                                         'mad': W_MAD_PER_VERIFY}},
+        'cpu_baseline': None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(batch)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if mism == 0 else 3
+
+
+if __name__ == '__main__':
+    sys.exit(main())

@@ -77,6 +77,15 @@ struct Device {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
+// restores the caller's current HIP device on scope exit (torch shares it)
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() { (void)hipGetDevice(&prev); }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 std::mutex g_mu;
 std::vector<Device> g_devs;
 
@@ -164,6 +173,7 @@ extern "C" {
 
 int pv_init(uint32_t device_mask) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   int count = 0;
   hipError_t e = hipGetDeviceCount(&count);
   if (e != hipSuccess || count <= 0) return fail(PV_ENODEV, "no HIP device available (%s)", hipGetErrorString(e));
@@ -185,6 +195,7 @@ int pv_init(uint32_t device_mask) {
 
 void pv_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   for (auto& d : g_devs) release_device(d);
   g_devs.clear();
 }
@@ -193,6 +204,7 @@ const char* pv_last_error(void) { return g_err.c_str(); }
 
 int pv_device_count(void) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   return (int)g_devs.size();
 }
 
@@ -200,6 +212,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
                     uint64_t n, uint8_t* verdict, uint32_t device_mask, uint32_t flags) {
   (void)flags;
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
   if (n == 0) return PV_OK;
   if (!pk || !sig || !msg_off || !verdict || (!msg_blob && msg_off[n] != msg_off[0]))
@@ -244,6 +257,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
 int pv_verify_batch_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off,
                            uint64_t n, uint8_t* verdict, uint64_t* bitmap, int device, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (n == 0) return PV_OK;
@@ -260,6 +274,7 @@ int pv_time_verify_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
                           uint64_t n, uint8_t* verdict, uint64_t* bitmap, int device, void* stream, int iters,
                           float* ms_hash, float* ms_curve) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (iters <= 0) return fail(PV_EINVAL, "iters must be > 0");
@@ -278,6 +293,7 @@ int pv_time_verify_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
 int pv_tally_device(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
                     uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached, int device, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (n_nodes == 0 || n_nodes > 1024) return fail(PV_EINVAL, "n_nodes must be in 1..1024");
@@ -291,6 +307,7 @@ int pv_tally_device(const uint8_t* verdict, const uint32_t* sender, const uint64
 int pv_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
              uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
   if (n_nodes == 0 || n_nodes > 1024) return fail(PV_EINVAL, "n_nodes must be in 1..1024");
   if (n_batches == 0) return PV_OK;
@@ -324,6 +341,7 @@ int pv_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* bat
 int pv_sign_batch_device(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n,
                          uint8_t* pk_out, uint8_t* sig_out, int device, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (n == 0) return PV_OK;
@@ -337,6 +355,7 @@ int pv_sign_batch_device(const uint8_t* seeds, const uint8_t* msg_blob, const ui
 int pv_sign_batch(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n,
                   uint8_t* pk_out, uint8_t* sig_out) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
   if (n == 0) return PV_OK;
   if (!seeds || !msg_off || !pk_out || !sig_out) return fail(PV_EINVAL, "null buffer");
@@ -365,6 +384,7 @@ int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, 
                     uint8_t* blob, uint8_t* seeds, uint8_t* pk, uint8_t* sig, uint8_t* tamper, int device,
                     void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (!off || !blob || !seeds || !pk || !sig || !tamper) return fail(PV_EINVAL, "null device buffer");

@@ -51,7 +51,7 @@ class PlenumGpuError(RuntimeError):
 
 _lib = None
 _lock = threading.Lock()
-_inited = False
+_inited_mask = None   # None = nothing initialised; 0 = every visible device
 
 
 def load():
@@ -76,20 +76,23 @@ def _check(fn, rc):
 
 
 def ensure_init(device_mask=0):
-    """pv_init once per process; raises PlenumGpuError when no GPU is usable."""
-    global _inited
+    """pv_init for the devices in device_mask (0 = all visible) unless already
+    initialised; raises PlenumGpuError when no GPU is usable."""
+    global _inited_mask
     with _lock:
-        if not _inited:
-            _check('pv_init', load().pv_init(device_mask))
-            _inited = True
+        if _inited_mask == 0 or (_inited_mask is not None and device_mask and
+                                 (device_mask & _inited_mask) == device_mask):
+            return
+        _check('pv_init', load().pv_init(device_mask))
+        _inited_mask = 0 if device_mask == 0 else (device_mask | (_inited_mask or 0))
 
 
 def shutdown():
-    global _inited
+    global _inited_mask
     with _lock:
         if _lib is not None:
             _lib.pv_shutdown()
-        _inited = False
+        _inited_mask = None
 
 
 def _ptr(a):

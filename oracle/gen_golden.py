@@ -640,7 +640,7 @@ def main():
     with open(os.path.join(OUT, 'kat.json'), 'w') as fh:
         json.dump(gen_kat(), fh, indent=1, sort_keys=True)
     with open(os.path.join(OUT, 'plenum_requests.json'), 'w') as fh:
-        json.dump(gen_plenum_requests(), fh, indent=0, sort_keys=True)
+        json.dump(gen_plenum_requests(), fh, indent=0)  # keep dict order: the signature loop order matters
     np.savez_compressed(os.path.join(OUT, 'raw_vectors.npz'), **gen_raw())
     np.savez_compressed(os.path.join(OUT, 'adversarial.npz'), **gen_adversarial())
     np.savez_compressed(os.path.join(OUT, 'tally.npz'), **gen_tally())

@@ -1,0 +1,86 @@
+"""The C-ABI library builds, loads on a CPU-only host, exports exactly what
+include/plenum_verify.h declares, and fails loudly without a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO
+
+HEADER = os.path.join(REPO, 'include', 'plenum_verify.h')
+
+
+def declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r'^\s*(?:int|void|const char \*)\s*\**\s*(pv_\w+)\s*\(', text, re.M)))
+
+
+@pytest.fixture(scope='module')
+def native():
+    import sys
+    sys.path.insert(0, PKG)
+    import build as pkg_build
+    pkg_build.build()
+    from plenum_gpu import _native
+    return _native
+
+
+def test_exports_every_declared_symbol(native):
+    names = declared()
+    assert len(names) >= 12
+    out = subprocess.run(['nm', '-D', '--defined-only', native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r' T (pv_\w+)', out))
+    assert set(names) <= exported, set(names) - exported
+    lib = native.load()
+    for n in names:
+        assert getattr(lib, n) is not None
+
+
+def test_python_binding_matches_header(native):
+    assert sorted(n for n, _, _ in native.SIGNATURES) == declared()
+
+
+def test_library_is_gfx950(native):
+    out = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-readelf', '--notes', native.LIB_PATH],
+                         capture_output=True, text=True)
+    blob = open(native.LIB_PATH, 'rb').read()
+    assert b'gfx950' in blob
+
+
+def _gpu_present(native):
+    rc = native.load().pv_init(0)
+    if rc == 0:
+        native.load().pv_shutdown()
+        return True
+    return False
+
+
+def test_fails_loudly_without_gpu(native):
+    if _gpu_present(native):
+        pytest.skip('a GPU is present; the no-GPU contract is exercised on CPU hosts')
+    lib = native.load()
+    assert lib.pv_init(0) == -19  # PV_ENODEV
+    assert lib.pv_last_error()
+    n = 1
+    buf = np.zeros(64, np.uint8)
+    off = np.zeros(2, np.uint64)
+    v = np.zeros(1, np.uint8)
+    p = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    assert lib.pv_verify_batch(p(buf), p(buf), p(buf), p(off), n, p(v), 0, 0) == -77  # PV_ENOTINIT
+    with pytest.raises(native.PlenumGpuError):
+        native.verify_batch_arrays(np.zeros((1, 32), np.uint8), np.zeros((1, 64), np.uint8),
+                                   np.zeros(0, np.uint8), np.zeros(2, np.uint64))
+
+
+def test_no_cpu_fallback_in_product_package():
+    """The product package never imports the oracle or the host build."""
+    pkg = os.path.join(PKG, 'plenum_gpu')
+    for fn in os.listdir(pkg):
+        if fn.endswith('.py'):
+            src = open(os.path.join(pkg, fn)).read()
+            assert 'oracle' not in src.lower().replace('libsodium', ''), fn
+            assert 'hostcheck' not in src, fn
+            assert 'libsodium.so' not in src, fn

@@ -1,0 +1,119 @@
+"""Parity of the HIP verify path (through the C-ABI) with the libsodium-1.0.18
+golden fixtures and the oracle; size-independent properties at full size."""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as orc
+from conftest import split_sm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def nat():
+    from plenum_gpu import _native
+    _native.ensure_init()
+    return _native
+
+
+def test_raw_vectors_bit_exact(nat, raw_vectors):
+    r = raw_vectors
+    got = nat.verify_batch_arrays(r['pk'], r['sig'], r['blob'], r['off'])
+    assert (got == r['verdict'].astype(bool)).all()
+
+
+def test_adversarial_bit_exact(nat, adversarial):
+    from plenum_gpu.nacl_wrappers import verify_signed_batch
+    rows = split_sm(adversarial)
+    got = verify_signed_batch([(pk, sm) for _, pk, sm, _ in rows])
+    wrong = [rows[k][0] for k in range(len(rows)) if got[k] != rows[k][3]]
+    assert not wrong, wrong
+
+
+def test_tally_fixture_verdicts(nat, tally_fx):
+    t = tally_fx
+    got = nat.verify_batch_arrays(t['pk'], t['sig'], t['blob'], t['off'])
+    assert (got == t['verdict'].astype(bool)).all()
+
+
+def test_empty_and_single(nat, raw_vectors):
+    r = raw_vectors
+    assert nat.verify_batch_arrays(np.zeros((0, 32), np.uint8), np.zeros((0, 64), np.uint8),
+                                   np.zeros(0, np.uint8), np.zeros(1, np.uint64)).size == 0
+    for i in (0, 1, 2):
+        o = r['off']
+        got = nat.verify_batch_arrays(r['pk'][i:i + 1], r['sig'][i:i + 1], r['blob'][int(o[i]):int(o[i + 1])],
+                                      np.array([0, o[i + 1] - o[i]], np.uint64))
+        assert got[0] == bool(r['verdict'][i])
+
+
+def test_random_ragged_vs_oracle(nat):
+    rng = np.random.default_rng(2026)
+    n = 6000
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = [rng.integers(0, 256, int(rng.choice([0, 1, 47, 48, 175, 176, int(rng.integers(0, 5000))])),
+                         dtype=np.uint8).tobytes() for _ in range(n)]
+    blob, off = nat.pack_messages(msgs)
+    pk, sig = nat.sign_batch_arrays(seeds, blob, off)
+    # corrupt ~10 %: random bit anywhere in R, S or M
+    for i in rng.choice(n, n // 10, replace=False):
+        which = rng.integers(0, 3)
+        if which == 0 or len(msgs[i]) == 0:
+            sig[i, rng.integers(0, 64)] ^= 1 << int(rng.integers(0, 8))
+        else:
+            m = bytearray(msgs[i])
+            m[rng.integers(0, len(m))] ^= 1 << int(rng.integers(0, 8))
+            msgs[i] = bytes(m)
+    blob, off = nat.pack_messages(msgs)
+    got = nat.verify_batch_arrays(pk, sig, blob, off)
+    want = orc.verify_batch(pk, sig, blob, off)
+    assert (got == want).all()
+    assert 0.05 < (~got).mean() < 0.15
+
+
+def test_batch_larger_than_persistent_grid(nat):
+    """More signatures than resident curve lanes: grid-stride loop and bitmap words."""
+    from plenum_gpu import synth
+    n = 300_000
+    rng = np.random.default_rng(3)
+    seeds = np.repeat(rng.integers(0, 256, (1000, 32), dtype=np.uint8), n // 1000, axis=0)
+    blob = rng.integers(0, 256, n * 64, dtype=np.uint8)
+    off = np.arange(n + 1, dtype=np.uint64) * 64
+    pk, sig = nat.sign_batch_arrays(seeds, blob, off)
+    bad = rng.choice(n, 5000, replace=False)
+    sig[bad, 40] ^= 4
+    got = nat.verify_batch_arrays(pk, sig, blob, off)
+    want = np.ones(n, bool)
+    want[bad] = False
+    assert (got == want).all()
+
+
+def test_invalid_arguments_raise(nat):
+    with pytest.raises(ValueError):
+        nat.verify_batch_arrays(np.zeros((2, 32), np.uint8), np.zeros((1, 64), np.uint8), np.zeros(0, np.uint8),
+                                np.zeros(3, np.uint64))
+    with pytest.raises(nat.PlenumGpuError):
+        nat.verify_batch_arrays(np.zeros((2, 32), np.uint8), np.zeros((2, 64), np.uint8), np.zeros(10, np.uint8),
+                                np.array([0, 8, 4], np.uint64))
+
+
+def test_multi_device_mask_shards(nat, raw_vectors):
+    """device_mask = every initialised device (one box: 1 GPU) gives the same verdicts."""
+    r = raw_vectors
+    got = nat.verify_batch_arrays(r['pk'], r['sig'], r['blob'], r['off'], device_mask=0)
+    assert (got == r['verdict'].astype(bool)).all()
+
+
+def test_sign_matches_oracle_and_fixture(nat, raw_vectors):
+    import hashlib
+    import struct
+    r = raw_vectors
+    idx = [i for i in range(len(r['verdict'])) if not r['tampered'][i]][:1500]
+    seeds = np.stack([np.frombuffer(hashlib.sha512(b'plenum-gpu/rawkey' + struct.pack('<Q', i % 2500)).digest()[:32],
+                                    np.uint8) for i in idx])
+    msgs = [r['blob'][int(r['off'][i]):int(r['off'][i + 1])].tobytes() for i in idx]
+    blob, off = nat.pack_messages(msgs)
+    pk, sig = nat.sign_batch_arrays(seeds, blob, off)
+    assert (pk == r['pk'][idx]).all() and (sig == r['sig'][idx]).all()

@@ -1,0 +1,125 @@
+// HOST INSTRUMENTATION BUILD of the kernel algorithms (test tooling only —
+// never loaded by the product package, see tests/test_hostcheck.py).
+//
+// Compiles indy-plenum_amd/csrc/pv_verify_core.h with g++ so that the exact
+// per-lane schedule the HIP kernels run can be
+//   * bound-checked: every fe_mul/fe_sq input is asserted to be LOOSE,
+//   * op-counted: field mul/sq/add/carry, SHA-512 blocks, scalar reductions
+//     per verify (the roofline's algorithmic work),
+//   * run under ASan/UBSan and gdb (no GPU needed).
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static uint64_t g_cnt[8];
+enum { HC_mul, HC_sq, HC_add, HC_carry, HC_sha, HC_sc };
+static int g_bad_bound = 0;
+
+#define PV_HD static inline
+#define PV_COUNT(kind) (++g_cnt[HC_##kind])
+#define PV_CHECK_LOOSE(f)                                                       \
+  do {                                                                          \
+    for (int i_ = 0; i_ < 10; ++i_) {                                           \
+      const uint32_t lim_ = (i_ & 1) ? 109000000u : 218000000u;                 \
+      if ((f).v[i_] > lim_) {                                                   \
+        if (!g_bad_bound)                                                       \
+          fprintf(stderr, "bound violation limb %d = %u > %u\n", i_, (f).v[i_], lim_); \
+        g_bad_bound = 1;                                                        \
+      }                                                                         \
+    }                                                                           \
+  } while (0)
+
+#include "../../indy-plenum_amd/csrc/pv_verify_core.h"
+
+using namespace pv;
+
+static uint32_t g_btab[BT_ENTRIES * BT_WORDS];
+static int g_btab_ready = 0;
+
+static void ensure_btab() {
+  if (g_btab_ready) return;
+  for (int k = 0; k < BT_ENTRIES; ++k) btable_entry(g_btab + k * BT_WORDS, k);
+  g_btab_ready = 1;
+}
+
+extern "C" {
+
+// verdicts with exactly the kernel's algorithm; the message blob must have
+// >= 16 readable bytes after the last message (same contract as the kernel)
+void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
+                     uint8_t* verdict) {
+  ensure_btab();
+  uint32_t atab[AT_WORDS];
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t h[8];
+    const bool pre = hash_one(h, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+    verdict[i] = pre && curve_one(pk + 32 * i, sig + 64 * i, h, atab, g_btab);
+  }
+}
+
+void hc_sign_batch(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* pk,
+                   uint8_t* sig) {
+  ensure_btab();
+  for (uint64_t i = 0; i < n; ++i) sign_one(pk + 32 * i, sig + 64 * i, seeds + 32 * i, blob + off[i],
+                                            off[i + 1] - off[i], g_btab);
+}
+
+void hc_btable(uint32_t* out) {
+  ensure_btab();
+  memcpy(out, g_btab, sizeof g_btab);
+}
+
+void hc_reset_counts(void) {
+  memset(g_cnt, 0, sizeof g_cnt);
+  g_bad_bound = 0;
+}
+
+// counts[0..5] = mul, sq, add, carry, sha blocks, scalar reductions
+int hc_get_counts(uint64_t* counts) {
+  for (int i = 0; i < 6; ++i) counts[i] = g_cnt[i];
+  return g_bad_bound;
+}
+
+// field self-test helpers: c = a*b, c = a^2 from/to canonical 32-byte encodings
+void hc_fe_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  uint32_t wa[8], wb[8], wo[8];
+  load8(wa, a); load8(wb, b);
+  fe fa, fb, fc;
+  fe_frombytes_w(fa, wa); fe_frombytes_w(fb, wb);
+  fe_mul(fc, fa, fb);
+  fe_tobytes_w(wo, fc);
+  store8(out, wo);
+}
+void hc_fe_sq(const uint8_t* a, uint8_t* out) {
+  uint32_t wa[8], wo[8];
+  load8(wa, a);
+  fe fa, fc;
+  fe_frombytes_w(fa, wa);
+  fe_sq(fc, fa);
+  fe_tobytes_w(wo, fc);
+  store8(out, wo);
+}
+void hc_fe_invert(const uint8_t* a, uint8_t* out) {
+  uint32_t wa[8], wo[8];
+  load8(wa, a);
+  fe fa, fc;
+  fe_frombytes_w(fa, wa);
+  fe_invert(fc, fa);
+  fe_tobytes_w(wo, fc);
+  store8(out, wo);
+}
+void hc_sc_reduce64(const uint8_t* in64, uint8_t* out32) {
+  uint32_t x[16], r[8];
+  memcpy(x, in64, 64);
+  sc_reduce64(r, x);
+  memcpy(out32, r, 32);
+}
+void hc_sc_muladd(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out) {
+  uint32_t wa[8], wb[8], wc[8], wo[8];
+  memcpy(wa, a, 32); memcpy(wb, b, 32); memcpy(wc, c, 32);
+  sc_muladd(wo, wa, wb, wc);
+  memcpy(out, wo, 32);
+}
+
+}  // extern "C"
