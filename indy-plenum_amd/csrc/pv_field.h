@@ -27,6 +27,17 @@
 #ifndef PV_CHECK_LOOSE
 #define PV_CHECK_LOOSE(f)
 #endif
+// Keeps the scheduler from interleaving consecutive field multiplies: each
+// one has 10 independent accumulator chains (enough ILP), and interleaving
+// several multiplies multiplies the live 64-bit accumulators (register
+// pressure -> occupancy).  Device-only builtin; empty in host builds.
+#ifndef PV_FE_FENCE
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PV_FE_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define PV_FE_FENCE()
+#endif
+#endif
 
 namespace pv {
 
@@ -99,6 +110,7 @@ PV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
     }
   }
   fe_carry_wide(h, acc);
+  PV_FE_FENCE();
 }
 
 // h = f^2 with the symmetric cross terms folded (55 products instead of 100).
@@ -136,6 +148,7 @@ PV_HD void fe_sq(fe& h, const fe& f) {
     }
   }
   fe_carry_wide(h, acc);
+  PV_FE_FENCE();
 }
 
 PV_HD void fe_sqn(fe& h, const fe& f, int n) {
