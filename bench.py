@@ -40,9 +40,12 @@ CFG = 2
 # Algorithmic work of the curve kernel per verify, counted by the host
 # instrumentation build of the same code (tests/test_hostcheck.py pins these):
 # field multiplies x 100 + squarings x 55 v_mad_u64_u32 (radix 2^25.5 schoolbook).
-W_MUL_PER_VERIFY = 1588
-W_SQ_PER_VERIFY = 1517
-W_MAD_PER_VERIFY = W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55
+# (the final Z^-1 is shared by CURVE_K = 4 signatures per lane: 3 of every 4
+# 254-squaring inversions are replaced by 3 multiplies; the decompression
+# multiplies by sqrt(-1) for about half of all keys, hence the .5)
+W_MUL_PER_VERIFY = 1581.5
+W_SQ_PER_VERIFY = 1326.5
+W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
 # v_mad_u64_u32 issue rate of one MI355X measured by tools/ubench/int_rates.hip
 # (profiles/r01_int_rates.json): lane-ops/s over the whole chip.
 P_MAD_PER_S = 2.7875e13

@@ -44,37 +44,42 @@ def _run(cmd):
     return r.stdout + r.stderr
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, defines=(), lib=None):
+    """Compile the library; `defines`/`lib` build named variants for A/B timing."""
     os.makedirs(LIBDIR, exist_ok=True)
-    stamp = LIB + '.stamp'
-    dig = _digest()
-    if not force and os.path.exists(LIB) and os.path.exists(stamp):
+    lib = lib or LIB
+    extra = ['-D' + d for d in defines]
+    stamp = lib + '.stamp'
+    dig = _digest() + ' '.join(extra)
+    if not force and os.path.exists(lib) and os.path.exists(stamp):
         with open(stamp) as fh:
             if fh.read().strip() == dig:
-                return LIB
+                return lib
     objs = []
     cmds = []
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, src + '.o')
+        obj = os.path.join(LIBDIR, os.path.basename(lib) + '.' + src + '.o')
         lang = ['-x', 'hip'] if src.endswith('.hip') else []
-        cmds.append([HIPCC] + COMMON + lang + ['-c', os.path.join(CSRC, src), '-o', obj])
+        cmds.append([HIPCC] + COMMON + extra + lang + ['-c', os.path.join(CSRC, src), '-o', obj])
         objs.append(obj)
     with ThreadPoolExecutor(len(cmds)) as ex:
         for out in ex.map(_run, cmds):
             if verbose and out.strip():
                 print(out)
-    tmp = LIB + '.tmp'
+    tmp = lib + '.tmp'
     _run([HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', tmp] + objs)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     with open(stamp, 'w') as fh:
         fh.write(dig)
-    return LIB
+    return lib
 
 
 if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--force', action='store_true')
     ap.add_argument('-v', '--verbose', action='store_true')
+    ap.add_argument('-D', dest='defines', action='append', default=[], help='extra -D for a variant build')
+    ap.add_argument('-o', dest='lib', default=None, help='output .so for a variant build')
     a = ap.parse_args()
-    print(build(force=a.force, verbose=a.verbose))
+    print(build(force=a.force, verbose=a.verbose, defines=a.defines, lib=a.lib))
     sys.exit(0)

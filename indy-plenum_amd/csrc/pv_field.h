@@ -153,6 +153,7 @@ PV_HD void fe_sq(fe& h, const fe& f) {
 
 PV_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
+#pragma unroll 1
   for (int i = 1; i < n; ++i) fe_sq(h, h);
 }
 

@@ -10,8 +10,9 @@ namespace pv {
 // base-point table: 129 niels entries (k*B, k = 0..128), 32 words each
 constexpr int BTAB_ENTRIES = 129;
 constexpr int BTAB_WORDS = 32;
-// per-lane A table: 9 cached entries (k*(-A), k = 0..8), 40 words each
-constexpr int ATAB_WORDS = 9 * 40;
+// per-lane scratch: A table (9 cached entries k*(-A), 40 words each) + the
+// CURVE_K points awaiting the shared inversion (40 words each)
+constexpr int ATAB_WORDS = 9 * 40 + 4 * 40;
 constexpr int CURVE_BLOCK = 256;
 constexpr int HASH_BLOCK = 256;
 

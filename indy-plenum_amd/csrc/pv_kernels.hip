@@ -17,7 +17,13 @@
 
 namespace pv {
 
-static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && AT_WORDS == ATAB_WORDS, "table layout");
+// waves per SIMD the curve kernel is compiled for (register budget 512 / w);
+// its hot Horner loop needs ~165 VGPRs, so 3 waves/SIMD keeps it spill-free
+#ifndef PV_CURVE_WAVES
+#define PV_CURVE_WAVES 3
+#endif
+
+static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS, "table layout");
 
 // ------------------------------------------------------------- hash kernel
 __global__ __launch_bounds__(HASH_BLOCK) void k_hash(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
@@ -53,33 +59,35 @@ hipError_t launch_btable_init(uint32_t* btab, hipStream_t s) {
 }
 
 // ------------------------------------------------------------ curve kernel
-// Persistent grid: lane gid owns scratch slot gid (its A table) and walks
-// signatures gid, gid + nthreads, ...  Each wavefront covers 64 consecutive
-// signatures per step, so its ballot is one aligned bitmap word.
-__global__ __launch_bounds__(CURVE_BLOCK) void k_curve(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
-                                                        const uint32_t* __restrict__ hin,
-                                                        const uint8_t* __restrict__ pre,
-                                                        const uint32_t* __restrict__ btab_g,
-                                                        uint32_t* __restrict__ scratch, uint8_t* __restrict__ verdict,
-                                                        uint64_t* __restrict__ bitmap, uint64_t n) {
+// Persistent grid: lane gid owns scratch slot gid (its A table and the
+// points awaiting the shared inversion) and takes CURVE_K signatures per round:
+// gid, gid + nthreads, ... , gid + (K-1) nthreads.  Each wavefront covers 64
+// consecutive signatures per k, so each ballot is one aligned bitmap word.
+__global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uint8_t* __restrict__ pk,
+                                                                        const uint8_t* __restrict__ sig,
+                                                                        const uint32_t* __restrict__ hin,
+                                                                        const uint8_t* __restrict__ pre,
+                                                                        const uint32_t* __restrict__ btab_g,
+                                                                        uint32_t* __restrict__ scratch,
+                                                                        uint8_t* __restrict__ verdict,
+                                                                        uint64_t* __restrict__ bitmap, uint64_t n) {
   __shared__ uint32_t btab[BTAB_ENTRIES * BTAB_WORDS];
   for (int j = threadIdx.x; j < BTAB_ENTRIES * BTAB_WORDS; j += CURVE_BLOCK) btab[j] = btab_g[j];
   __syncthreads();
   const uint64_t nthreads = (uint64_t)gridDim.x * CURVE_BLOCK;
   const uint64_t gid = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
-  uint32_t* atab = scratch + gid * ATAB_WORDS;
-  for (uint64_t base = 0; base < n; base += nthreads) {
-    const uint64_t i = base + gid;
-    bool ok = false;
-    if (i < n && pre[i]) {
-      uint32_t hh[8];
-      load8(hh, reinterpret_cast<const uint8_t*>(hin + 8 * i));
-      ok = curve_one(pk + 32 * i, sig + 64 * i, hh, atab, btab);
-    }
-    const uint64_t ball = __ballot(ok);
-    if (i < n) {
-      verdict[i] = ok ? 1 : 0;
-      if ((threadIdx.x & 63) == 0) bitmap[i >> 6] = ball;
+  uint32_t* lane = scratch + gid * LANE_WORDS;
+  for (uint64_t base = 0; base < n; base += CURVE_K * nthreads) {
+    const uint32_t okm = curve_group(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab);
+#pragma unroll
+    for (int k = 0; k < CURVE_K; ++k) {
+      const uint64_t i = base + (uint64_t)k * nthreads + gid;
+      const bool ok = (okm >> k) & 1u;
+      const uint64_t ball = __ballot(ok);
+      if (i < n) {
+        verdict[i] = ok ? 1 : 0;
+        if ((threadIdx.x & 63) == 0) bitmap[i >> 6] = ball;
+      }
     }
   }
 }
@@ -93,7 +101,7 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  uint64_t need = (n + CURVE_BLOCK - 1) / CURVE_BLOCK;
+  uint64_t need = (n + (uint64_t)CURVE_BLOCK * CURVE_K - 1) / ((uint64_t)CURVE_BLOCK * CURVE_K);
   uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
   if (b * CURVE_BLOCK > scratch_lanes) b = scratch_lanes / CURVE_BLOCK;
   if (b == 0) return hipErrorInvalidValue;

@@ -181,18 +181,67 @@ PV_HD void btable_entry(uint32_t* p, int k) {
   p[31] = 0;
 }
 
+// ------------------------------------------- table-operand point additions
+// r = p + s*Q with Q read straight from a table entry (`q`), one field element
+// at a time right before the multiply that consumes it.  The sign is applied
+// by choosing WHICH of Y+X / Y-X to load and negating the C term, so no
+// 10-limb copies are made: this keeps the hot loop inside 3 waves/SIMD of
+// registers.  Same formulas as ge_add_cached / ge_madd (add-2008-hwcd-3).
+PV_HD void ge_add_cached_at(ge_p1p1& r, const ge_p3& p, const uint32_t* q, bool neg) {
+  fe c, d, a, b, u, g;
+  load_fe(g, q + 30);             // 2d*T2
+  fe_mul(c, g, p.T);
+  load_fe(g, q + 20);             // 2*Z2
+  fe_mul(d, p.Z, g);
+  fe_add(u, p.Y, p.X);
+  load_fe(g, q + (neg ? 10 : 0)); // Y2+X2 (Y2-X2 for -Q)
+  fe_mul(a, u, g);
+  fe_sub(u, p.Y, p.X);
+  load_fe(g, q + (neg ? 0 : 10));
+  fe_mul(b, u, g);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_neg(u, c);                   // -Q: C -> -C
+  fe_cmov(c, c, u, neg);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);
+}
+
+PV_HD void ge_madd_at(ge_p1p1& r, const ge_p3& p, const uint32_t* q, bool neg) {
+  fe c, d, a, b, u, g;
+  load_fe(g, q + 20);             // 2d*x2*y2
+  fe_mul(c, g, p.T);
+  fe_add(d, p.Z, p.Z);
+  fe_carry(d);
+  fe_add(u, p.Y, p.X);
+  load_fe(g, q + (neg ? 10 : 0)); // y2+x2 (y2-x2 for -Q)
+  fe_mul(a, u, g);
+  fe_sub(u, p.Y, p.X);
+  load_fe(g, q + (neg ? 0 : 10));
+  fe_mul(b, u, g);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_neg(u, c);
+  fe_cmov(c, c, u, neg);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);
+}
+
 // ----------------------------------------------------------------- curve
 // cached multiples 0..8 of P into a per-lane table (9 x 40 words)
 PV_HD void build_atab(uint32_t* atab, const ge_p3& P) {
-  ge_cached c1, c;
+  ge_cached c;
   ge_cached_identity(c);
   store_cached(atab, c);
-  ge_p3_to_cached(c1, P);
-  store_cached(atab + AT_ENTRY, c1);
+  ge_p3_to_cached(c, P);
+  store_cached(atab + AT_ENTRY, c);
   ge_p3 prev = P;
-  ge_p1p1 t;
 #pragma unroll 1
   for (int k = 2; k <= 8; ++k) {
+    // re-read 1*P from the table instead of keeping it live (register budget)
+    ge_cached c1;
+    load_cached(c1, atab + AT_ENTRY);
+    ge_p1p1 t;
     ge_add_cached(t, prev, c1, false);
     ge_p1p1_to_p3(prev, t);
     ge_p3_to_cached(c, prev);
@@ -213,15 +262,27 @@ PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss
   ge_p3_0(acc);
   ge_p1p1 t;
   ge_p2 r2;
+  // Digits are consumed from the top word down.  The current words sit in
+  // hw/sw; at each 8-window boundary the arrays shift by one word with static
+  // indices only (a wave-uniform dynamic index would make the compiler spill
+  // hp/sp to scratch).
+  uint32_t hw = hp[7], sw = sp[7];
   {
-    const int dA = (int)(hp[7] >> 28) - 8;
-    ge_cached c;
-    load_cached(c, atab + (dA < 0 ? -dA : dA) * AT_ENTRY);
-    ge_add_cached(t, acc, c, dA < 0);
+    const int dA = (int)(hw >> 28) - 8;
+    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
     ge_p1p1_to_p2(r2, t);
   }
 #pragma unroll 1
   for (int i = 62; i >= 0; --i) {
+    if ((i & 7) == 7) {
+#pragma unroll
+      for (int k = 7; k > 0; --k) {
+        hp[k] = hp[k - 1];
+        sp[k] = sp[k - 1];
+      }
+      hw = hp[7];
+      sw = sp[7];
+    }
 #pragma unroll 1
     for (int k = 0; k < 3; ++k) {
       ge_p2_dbl(t, r2);
@@ -229,45 +290,114 @@ PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss
     }
     ge_p2_dbl(t, r2);
     ge_p1p1_to_p3(acc, t);
-    const uint32_t hw = pick8(hp, i >> 3);
     const int dA = (int)((hw >> (4 * (i & 7))) & 15u) - 8;
-    {
-      ge_cached c;
-      load_cached(c, atab + (dA < 0 ? -dA : dA) * AT_ENTRY);
-      ge_add_cached(t, acc, c, dA < 0);
-    }
+    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
     if ((i & 1) == 0) {
-      const uint32_t sw = pick8(sp, i >> 3);
       const int dB = (int)((sw >> (8 * ((i >> 1) & 3))) & 255u) - 128;
       ge_p1p1_to_p3(acc, t);
-      ge_niels q;
-      load_niels(q, btab + (dB < 0 ? -dB : dB) * BT_WORDS);
-      ge_madd(t, acc, q, dB < 0);
+      ge_madd_at(t, acc, btab + (dB < 0 ? -dB : dB) * BT_WORDS, dB < 0);
     }
     ge_p1p1_to_p2(r2, t);
   }
   out = r2;
 }
 
-// decompress A, R' = h(-A) + S B, encode(R') == R.  `atab` is this lane's
-// 360-word scratch; `btab` the base-point table (LDS in the kernel).
-PV_HD bool curve_one(const uint8_t* pk, const uint8_t* sig, const uint32_t hh[8], uint32_t* atab,
-                     const uint32_t* btab) {
-  uint32_t A[8], R[8], S[8];
-  load8(A, pk);
-  load8(R, sig);
-  load8(S, sig + 32);
+// decompress A and compute R' = h(-A) + S B (projective, not yet encoded).
+// `atab` is this lane's table scratch; `btab` the base-point table (LDS in the
+// kernel).  Inputs are loaded right where they are consumed so that no
+// 32-byte value stays live across the whole verification (register budget of
+// the hot loop).  false = rejected before the final comparison.
+PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const uint32_t* hh_src, uint32_t* atab,
+                       const uint32_t* btab) {
   ge_p3 negA;
-  if (!ge_frombytes_negate(negA, A)) return false;
+  {
+    uint32_t A[8];
+    load8(A, pk);
+    if (!ge_frombytes_negate(negA, A)) return false;
+  }
   build_atab(atab, negA);
-  ge_p2 rp;
+  uint32_t hh[8], S[8];
+  load8(hh, reinterpret_cast<const uint8_t*>(hh_src));
+  load8(S, sig + 32);
   double_scalarmult(rp, hh, S, atab, btab);
-  uint32_t enc[8];
-  ge_p2_tobytes(enc, rp);
-  uint32_t diff = 0;
+  return true;
+}
+
+// Signatures one lane finishes together: their final Z^-1 share ONE field
+// inversion (Montgomery's trick: 3(K-1) multiplies + 1 inversion instead of
+// K inversions).
+constexpr int CURVE_K = 4;
+constexpr int PT_WORDS = 40;                        // X, Y, Z, prefix product
+constexpr int LANE_WORDS = AT_WORDS + CURVE_K * PT_WORDS;
+
+// in place over K entries of (X, Y, Z, P): Z_k <- Z_k^-1 (all Z_k != 0)
+PV_HD void batch_invert_z(uint32_t* pts, int K) {
+  fe acc, z, t;
+  load_fe(acc, pts + 20);
+  store_fe(pts + 30, acc);
+#pragma unroll 1
+  for (int k = 1; k < K; ++k) {
+    load_fe(z, pts + PT_WORDS * k + 20);
+    fe_mul(acc, acc, z);
+    store_fe(pts + PT_WORDS * k + 30, acc);
+  }
+  fe_invert(acc, acc);                              // (Z_0 ... Z_{K-1})^-1
+#pragma unroll 1
+  for (int k = K - 1; k > 0; --k) {
+    load_fe(t, pts + PT_WORDS * (k - 1) + 30);      // Z_0 ... Z_{k-1}
+    load_fe(z, pts + PT_WORDS * k + 20);
+    fe_mul(t, acc, t);                              // Z_k^-1
+    fe_mul(acc, acc, z);                            // (Z_0 ... Z_{k-1})^-1
+    store_fe(pts + PT_WORDS * k + 20, t);
+  }
+  store_fe(pts + 20, acc);
+}
+
+// One lane's group of CURVE_K signatures i0, i0 + stride, ...: returns the
+// accepted bitmask.  Rejected or absent entries carry Z = 1 through the
+// shared inversion.  scratch = LANE_WORDS words owned by this lane.
+PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre, uint64_t i0,
+                           uint64_t stride, uint64_t n, uint32_t* scratch, const uint32_t* btab) {
+  uint32_t* pts = scratch + AT_WORDS;
+  uint32_t live = 0;
+#pragma unroll 1
+  for (int k = 0; k < CURVE_K; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * stride;
+    ge_p2 rp;
+    bool ok = false;
+    if (i < n && pre[i]) ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 8 * i, scratch, btab);
+    if (!ok) {
+      fe_0(rp.X);
+      fe_0(rp.Y);
+      fe_1(rp.Z);
+    }
+    store_fe(pts + PT_WORDS * k, rp.X);
+    store_fe(pts + PT_WORDS * k + 10, rp.Y);
+    store_fe(pts + PT_WORDS * k + 20, rp.Z);
+    live |= (ok ? 1u : 0u) << k;
+  }
+  batch_invert_z(pts, CURVE_K);
+  uint32_t accepted = 0;
+#pragma unroll 1
+  for (int k = 0; k < CURVE_K; ++k) {
+    if (!((live >> k) & 1u)) continue;
+    const uint64_t i = i0 + (uint64_t)k * stride;
+    fe zi, x, y;
+    load_fe(zi, pts + PT_WORDS * k + 20);
+    load_fe(x, pts + PT_WORDS * k);
+    fe_mul(x, x, zi);
+    load_fe(y, pts + PT_WORDS * k + 10);
+    fe_mul(y, y, zi);
+    uint32_t enc[8], R[8];
+    fe_tobytes_w(enc, y);
+    enc[7] ^= fe_isnegative(x) << 31;
+    load8(R, sig + 64 * i);
+    uint32_t diff = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) diff |= enc[k] ^ R[k];
-  return diff == 0;
+    for (int w = 0; w < 8; ++w) diff |= enc[w] ^ R[w];
+    accepted |= (diff == 0 ? 1u : 0u) << k;
+  }
+  return accepted;
 }
 
 // ------------------------------------------------------------ batch signer

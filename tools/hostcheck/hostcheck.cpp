@@ -50,12 +50,17 @@ extern "C" {
 void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
                      uint8_t* verdict) {
   ensure_btab();
-  uint32_t atab[AT_WORDS];
-  for (uint64_t i = 0; i < n; ++i) {
-    uint32_t h[8];
-    const bool pre = hash_one(h, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
-    verdict[i] = pre && curve_one(pk + 32 * i, sig + 64 * i, h, atab, g_btab);
+  static uint32_t lane[LANE_WORDS];
+  uint32_t* h = (uint32_t*)calloc(n ? n * 8 : 8, sizeof(uint32_t));
+  uint8_t* pre = (uint8_t*)calloc(n ? n : 1, 1);
+  for (uint64_t i = 0; i < n; ++i)
+    pre[i] = hash_one(h + 8 * i, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+  for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
+    const uint32_t okm = curve_group(pk, sig, h, pre, i0, 1, n, lane, g_btab);
+    for (int k = 0; k < CURVE_K && i0 + k < n; ++k) verdict[i0 + k] = (okm >> k) & 1u;
   }
+  free(h);
+  free(pre);
 }
 
 void hc_sign_batch(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* pk,

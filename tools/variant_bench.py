@@ -1,0 +1,64 @@
+"""Interleaved A/B timing of library variants in ONE process (guide §5.4 rule 24).
+
+    python tools/variant_bench.py lib_a.so lib_b.so ... [--n N --rounds R]
+
+Each variant is loaded with its own ctypes handle, pv_init'ed, and times the
+verify kernels (HIP events on the launch stream) over the same device-resident
+synthetic C2 batch; verdicts must agree across variants.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'indy-plenum_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from plenum_gpu import _native as nat  # noqa: E402
+from plenum_gpu.device import SyntheticBatch, _p  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('libs', nargs='+')
+    ap.add_argument('--n', type=int, default=1_000_000)
+    ap.add_argument('--rounds', type=int, default=5)
+    a = ap.parse_args()
+    b = SyntheticBatch(0, a.n, 256)
+    torch.cuda.synchronize()
+    tamper = b.tamper.cpu().numpy().astype(bool)
+    libs = []
+    for path in a.libs:
+        lib = ctypes.CDLL(os.path.abspath(path))
+        for name, res, args in nat.SIGNATURES:
+            getattr(lib, name).restype = res
+            getattr(lib, name).argtypes = args
+        assert lib.pv_init(1) == 0, lib.pv_last_error()
+        libs.append((os.path.basename(path), lib))
+    res = {n: [] for n, _ in libs}
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for r in range(a.rounds):
+        for name, lib in libs:
+            h, c = ctypes.c_float(), ctypes.c_float()
+            b.verdict.zero_()
+            rc = lib.pv_time_verify_device(_p(b.pk), _p(b.sig), _p(b.blob), _p(b.off), a.n, _p(b.verdict),
+                                           _p(b.bitmap), 0, stream, 2, ctypes.byref(h), ctypes.byref(c))
+            assert rc == 0, lib.pv_last_error()
+            v = b.verdict.cpu().numpy().astype(bool)
+            assert (v == ~tamper).all(), name
+            res[name].append((h.value, c.value))
+    out = {}
+    for name, vals in res.items():
+        cs = sorted(v[1] for v in vals)
+        hs = sorted(v[0] for v in vals)
+        out[name] = {'curve_ms_median': cs[len(cs) // 2], 'curve_ms_min': cs[0], 'hash_ms_median': hs[len(hs) // 2],
+                     'verifies_per_s_kernel': a.n / ((cs[len(cs) // 2] + hs[len(hs) // 2]) * 1e-3)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == '__main__':
+    main()
