@@ -46,8 +46,9 @@ PV_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe_sq(xy2, t);               // (X+Y)^2
   fe_add(r.Y, yy, xx);         // LOOSE
   fe_sub(r.Z, yy, xx);         // LOOSE
-  fe_sub4(r.X, xy2, r.Y);      // (X+Y)^2 - X^2 - Y^2 = 2XY
-  fe_carry(r.X);
+  fe_sub4(r.X, xy2, r.Y);      // (X+Y)^2 - X^2 - Y^2 = 2XY, even limbs < 2^28.4:
+                               // only ever the FIRST operand of r.X*r.T / r.X*r.Y
+                               // (second operand TIGHT / LOOSE), so no carry needed
   fe_add(t, zz2, zz2);         // 2Z^2, even limbs <= 2^27
   fe_sub4(r.T, t, r.Z);
   fe_carry(r.T);

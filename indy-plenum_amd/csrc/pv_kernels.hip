@@ -18,15 +18,16 @@
 namespace pv {
 
 // waves per SIMD the curve kernel is compiled for (register budget 512 / w);
-// its hot Horner loop needs ~165 VGPRs, so 3 waves/SIMD keeps it spill-free
+// its hot Horner loop needs ~165 VGPRs; 2 waves/SIMD (<= 256 VGPRs) measured
+// fastest (tools/variant_bench.py: 2 > 3 > 4 waves once spills appear)
 #ifndef PV_CURVE_WAVES
-#define PV_CURVE_WAVES 3
+#define PV_CURVE_WAVES 2
 #endif
 
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS, "table layout");
 
 // ------------------------------------------------------------- hash kernel
-__global__ __launch_bounds__(HASH_BLOCK) void k_hash(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+__global__ __launch_bounds__(HASH_BLOCK, 2) void k_hash(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
                                                       const uint8_t* __restrict__ blob,
                                                       const uint64_t* __restrict__ off, uint64_t n,
                                                       uint32_t* __restrict__ hout, uint8_t* __restrict__ pre) {

@@ -54,10 +54,23 @@ _lock = threading.Lock()
 _inited_mask = None   # None = nothing initialised; 0 = every visible device
 
 
+def _bind_runtime_first():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own
+    libamdhip64.so.7 (same soname as /opt/rocm's); whichever is loaded first
+    serves every later NEEDED entry.  Loading torch's copy first keeps torch
+    usable in processes that also call this library (bench, multi-GPU ranks,
+    the device-pointer entry points); without torch, /opt/rocm's is used."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load():
     """Load the shared library (raises OSError if it was not built)."""
     global _lib
     if _lib is None:
+        _bind_runtime_first()
         if not os.path.exists(LIB_PATH):
             raise OSError('libplenum_verify.so not found at {} — build it with '
                           '`python indy-plenum_amd/build.py` (there is no CPU fallback)'.format(LIB_PATH))

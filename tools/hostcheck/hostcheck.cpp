@@ -18,17 +18,39 @@ static int g_bad_bound = 0;
 
 #define PV_HD static inline
 #define PV_COUNT(kind) (++g_cnt[HC_##kind])
-#define PV_CHECK_LOOSE(f)                                                       \
-  do {                                                                          \
-    for (int i_ = 0; i_ < 10; ++i_) {                                           \
-      const uint32_t lim_ = (i_ & 1) ? 109000000u : 218000000u;                 \
-      if ((f).v[i_] > lim_) {                                                   \
-        if (!g_bad_bound)                                                       \
-          fprintf(stderr, "bound violation limb %d = %u > %u\n", i_, (f).v[i_], lim_); \
-        g_bad_bound = 1;                                                        \
-      }                                                                         \
-    }                                                                           \
-  } while (0)
+static void hc_bad(const char* what, int k, unsigned long long v) {
+  if (!g_bad_bound) fprintf(stderr, "bound violation: %s [%d] = %llu\n", what, k, v);
+  g_bad_bound = 1;
+}
+// exact exactness conditions of fe_mul(f, g): 2 f_i < 2^32 (odd i),
+// 19 g_j < 2^32, every column sum (+ carry-in < 2^39) < 2^64
+static void hc_check_mul(const uint32_t* f, const uint32_t* g) {
+  for (int i = 1; i < 10; i += 2)
+    if (2ull * f[i] >= (1ull << 32)) hc_bad("2f", i, f[i]);
+  for (int j = 1; j < 10; ++j)
+    if (19ull * g[j] >= (1ull << 32)) hc_bad("19g", j, g[j]);
+  for (int k = 0; k < 10; ++k) {
+    unsigned __int128 s = (unsigned __int128)1 << 39;
+    for (int i = 0; i < 10; ++i) {
+      const int j = (k - i + 10) % 10;
+      unsigned __int128 t = (unsigned __int128)f[i] * g[j];
+      if ((i & 1) && (j & 1)) t *= 2;
+      if (i + j >= 10) t *= 19;
+      s += t;
+    }
+    if (s >> 64) hc_bad("column", k, (unsigned long long)(s >> 64));
+  }
+}
+// fe_sq(f): operands 4 f_odd, 19 f_j and the columns of f*f
+static void hc_check_sq(const uint32_t* f) {
+  for (int i = 1; i < 10; i += 2)
+    if (4ull * f[i] >= (1ull << 32)) hc_bad("4f", i, f[i]);
+  for (int j = 5; j < 10; ++j)
+    if (38ull * f[j] >= (1ull << 33)) hc_bad("19f", j, f[j]);
+  hc_check_mul(f, f);
+}
+#define PV_CHECK_MUL(f, g) hc_check_mul((f).v, (g).v)
+#define PV_CHECK_SQ(f) hc_check_sq((f).v)
 
 #include "../../indy-plenum_amd/csrc/pv_verify_core.h"
 
