@@ -46,21 +46,21 @@ CFG = 2
 W_MUL_PER_VERIFY = 1581.5
 W_SQ_PER_VERIFY = 1326.5
 W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
-# v_mad_u64_u32 issue rate of one MI355X measured by tools/ubench/int_rates.hip
-# (profiles/r01_int_rates.json): lane-ops/s over the whole chip.
-P_MAD_PER_S = 2.7875e13
+# v_mad_u64_u32 issue ceiling of one MI355X measured by tools/ubench/mad_peak.hip
+# (profiles/r01_mad_peak.json, best over 1..8 waves/SIMD): lane-ops/s, whole chip.
+P_MAD_PER_S = 3.3896e13
 
 
 def _mad_peak():
-    path = os.path.join(REPO, 'profiles', 'r01_int_rates.json')
+    """Best v_mad_u64_u32 lane-ops/s over 1..8 waves/SIMD (tools/ubench/mad_peak.hip,
+    profiles/r01_mad_peak.json): the chip's integer multiply-add issue ceiling."""
+    path = os.path.join(REPO, 'profiles', 'r01_mad_peak.json')
     try:
         with open(path) as fh:
-            for r in json.load(fh)['results']:
-                if r['insn'] == 'v_mad_u64_u32':
-                    return float(r['lane_ops_per_s'])
+            return max(float(r['lane_ops_per_s']) for r in json.load(fh)['results']
+                       if r['insn'] == 'v_mad_u64_u32')
     except (OSError, KeyError, ValueError):
-        pass
-    return P_MAD_PER_S
+        return P_MAD_PER_S
 
 
 def _traffic_per_launch():
