@@ -30,12 +30,24 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from plenum_gpu import _native as nat  # noqa: E402
-from plenum_gpu.device import SyntheticBatch  # noqa: E402
+from plenum_gpu import synth  # noqa: E402
+from plenum_gpu.device import SyntheticBatch, tally_device  # noqa: E402
+from plenum_gpu.quorums import Quorums  # noqa: E402
 
 METRIC = 'Ed25519 verifies/sec at 1/2/4/8 MI355X vs libsodium on host cores'
-N_PER_RANK = 1_000_000
-MLEN = 256
-CFG = 2
+# BASELINE.json configs as bench workloads (per rank; weak scaling).  c2 is the
+# headline (configs[1]); c3/c4 are the pool-tally and sharded mixed-payload cases.
+CONFIGS = {
+    'c2': dict(mode=synth.FIXED, n=1_000_000, cfg=2, mlen=256, mlen_max=256, key_mod=0,
+               workload='C2: 1M Ed25519 request signatures per GPU, distinct keys, 256 B payloads, ~5% tampered '
+                        '(BASELINE.json configs[1])'),
+    'c3': dict(mode=synth.COMMIT, n=2_500_000, cfg=3, mlen=0, mlen_max=0, key_mod=0, n_nodes=25,
+               workload='C3: 25-node pool (f=8), 100k 3PC batches of per-node COMMIT signatures per GPU, '
+                        'verify + n-f quorum tally (BASELINE.json configs[2])'),
+    'c4': dict(mode=synth.RANGE, n=8_000_000, cfg=4, mlen=128, mlen_max=4096, key_mod=1 << 20,
+               workload='C4: 64M signatures over 8 GPUs = 8M per GPU, payloads uniform 128 B-4 KB, key pool 2^20, '
+                        '~5% tampered, RCCL all-gather of verdict bitmaps (BASELINE.json configs[3])'),
+}
 
 # Algorithmic work of the curve kernel per verify, counted by the host
 # instrumentation build of the same code (tests/test_hostcheck.py pins these):
@@ -73,7 +85,7 @@ def _traffic_per_launch():
         return None
 
 
-def cpu_baseline(batch, seconds=1.5, sample=8192):
+def cpu_baseline(batch, workload, seconds=1.5, sample=8192):
     """libsodium crypto_sign_verify_detached on the host cores over the first
     `sample` signatures of this rank's workload (copied to host)."""
     so = os.path.join(REPO, 'oracle', 'liboracle.so')
@@ -112,7 +124,7 @@ def cpu_baseline(batch, seconds=1.5, sample=8192):
     return {'value': round(rate, 1), 'unit': 'verifies/s', 'cores': threads,
             'kind': 'reference' if kind.value == 0 else 'port',
             'sample': '{} ({} threads, {:.1f} s wall; 1 thread: {:.1f} verifies/s) over the first {} signatures '
-                      'of the C2 workload, host {}'.format(name, threads, seconds, rate1, sample, cpu)}
+                      'of the {} workload, host {}'.format(name, threads, seconds, rate1, sample, workload, cpu)}
 
 
 def main():
@@ -120,7 +132,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--n', type=int, default=N_PER_RANK, help='signatures per GPU (default: C2, 1M)')
+    ap.add_argument('--config', choices=sorted(CONFIGS), default='c2', help='workload (default c2, the headline)')
+    ap.add_argument('--n', type=int, default=None, help='signatures per GPU (default: the config\'s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -132,13 +145,28 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
 
-    n = args.n
-    batch = SyntheticBatch(local, n, MLEN, cfg=CFG, first=rank * n)
+    cfg = CONFIGS[args.config]
+    n = args.n or cfg['n']
+    n_nodes = cfg.get('n_nodes', 25)
+    if cfg['mode'] == synth.COMMIT:
+        n -= n % n_nodes
+    batch = SyntheticBatch(local, n, cfg['mlen'], cfg=cfg['cfg'], first=rank * n, key_mod=cfg['key_mod'],
+                           mode=cfg['mode'], mlen_max=cfg['mlen_max'], n_nodes=n_nodes)
     torch.cuda.synchronize()
     gathered = torch.zeros(world * batch.bitmap.numel(), dtype=torch.int64, device=dev) if world > 1 else None
+    tally = None
+    if cfg['mode'] == synth.COMMIT:
+        nb = n // n_nodes
+        q = Quorums(n_nodes).commit.value
+        tally = dict(nb=nb, q=q, boff=torch.arange(nb + 1, dtype=torch.int64, device=dev) * n_nodes,
+                     votes=torch.empty(nb, dtype=torch.int32, device=dev),
+                     reached=torch.empty(nb, dtype=torch.uint8, device=dev))
 
     def step():
         batch.verify()
+        if tally is not None:
+            tally_device(batch.verdict, batch.sender, tally['boff'], n_nodes, tally['q'], tally['votes'],
+                         tally['reached'])
         if world > 1:
             dist.all_gather_into_tensor(gathered, batch.bitmap)
 
@@ -167,6 +195,10 @@ def main():
     mism = int((verdict == tamper).sum())
     bits = np.unpackbits(batch.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
     mism += int((bits != verdict).sum())
+    if tally is not None:
+        want_votes, want_reached = synth.c3_expected(rank * tally['nb'], tally['nb'], n_nodes, tally['q'])
+        mism += int((tally['votes'].cpu().numpy() != want_votes.astype(np.int32)).sum())
+        mism += int((tally['reached'].cpu().numpy().astype(bool) != want_reached).sum())
     if world > 1:
         allbits = np.unpackbits(gathered.cpu().numpy().view(np.uint8), bitorder='little')
         per = batch.bitmap.numel() * 64
@@ -188,9 +220,10 @@ def main():
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3),
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',
         'data': 'synthetic (device-generated, deterministic: plenum_gpu/synth.py)',
-        'config': {'workload': 'C2: 1M Ed25519 request signatures per GPU, distinct keys, 256 B payloads, '
-                               '~5% tampered (BASELINE.json configs[1])',
-                   'signatures_per_gpu': n, 'msg_bytes': MLEN, 'tampered': int(tamper.sum()),
+        'config': {'workload': cfg['workload'], 'name': args.config,
+                   'signatures_per_gpu': n, 'msg_bytes': [cfg['mlen'], cfg['mlen_max']] if cfg['mlen'] != cfg['mlen_max']
+                   else cfg['mlen'], 'mean_msg_bytes': round(batch.blob_bytes / max(1, n), 1),
+                   'key_pool': cfg['key_mod'] or 'distinct', 'tampered': int(tamper.sum()),
                    'parallelism': 'dp{} (disjoint index shards) + RCCL all-gather of verdict bitmaps'.format(world)
                    if world > 1 else 'single GPU'},
         'verdict_mismatches': mism,
@@ -198,13 +231,18 @@ def main():
         'roofline': {'bound': 'valu', 'kernel': 'k_curve',
                      'achieved': round(achieved / 1e12, 3), 'peak': round(peak / 1e12, 3),
                      'unit': 'Tmad/s (v_mad_u64_u32 lane-ops)', 'frac': round(achieved / peak, 4),
-                     'traffic': _traffic_per_launch(),
+                     'traffic': _traffic_per_launch() if (args.config, n) == ('c2', CONFIGS['c2']['n']) else None,
                      'work_per_verify': {'fe_mul': W_MUL_PER_VERIFY, 'fe_sq': W_SQ_PER_VERIFY,
                                          'mad': W_MAD_PER_VERIFY}},
         'cpu_baseline': None,
     }
+    if tally is not None:
+        out['config']['batches_per_gpu'] = tally['nb']
+        out['config']['quorum'] = tally['q']
+        out['batches_per_s'] = round(world * tally['nb'] * args.steps / elapsed, 1)
+        out['quorum_reached'] = int(tally['reached'].sum().item())
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(batch)
+        out['cpu_baseline'] = cpu_baseline(batch, args.config.upper())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -111,9 +111,31 @@ int pv_sign_batch_device(const uint8_t *seeds, const uint8_t *msg_blob, const ui
                          uint8_t *pk_out, uint8_t *sig_out, int device, void *stream);
 
 /* Deterministic synthetic workload on the device (bench/tests; spec in
- * plenum_gpu/synth.py): fixed-length messages, seeds, tamper flags, signed,
- * tampered.  Outputs are device buffers the caller allocated:
- *   off (n+1), blob (n*mlen + 16), seeds (n*32), pk (n*32), sig (n*64), tamper (n). */
+ * plenum_gpu/synth.py).  Two phases so that the caller can
+ * size the message blob:
+ *   pv_synth_layout_device  off[0..n] <- exclusive prefix sum of the message
+ *                           lengths (off[n] = blob bytes)
+ *   pv_synth_fill_device    messages, seeds, tamper flags (and for COMMIT the
+ *                           sender node of every vote), then keygen + sign, then
+ *                           the spec's single-bit tampering.
+ * Modes: FIXED (C2: len = mlen_min), RANGE (C4: len uniform in [mlen_min,
+ * mlen_max]), COMMIT (C3: signature i is node slot i % n_nodes's COMMIT vote
+ * in 3PC batch i / n_nodes; M = "instId:0|op:COMMIT|ppSeqNo:<b+1>|viewNo:0").
+ * key_mod (FIXED/RANGE): key index = i % key_mod (0 = distinct keys).
+ * Buffers are device buffers the caller allocated: off (n+1), blob (off[n] + 16),
+ * seeds (n*32), pk (n*32), sig (n*64), tamper (n), sender (n or NULL). */
+#define PV_SYNTH_FIXED 0u
+#define PV_SYNTH_RANGE 1u
+#define PV_SYNTH_COMMIT 2u
+
+int pv_synth_layout_device(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t mlen_min,
+                           uint32_t mlen_max, uint32_t n_nodes, uint64_t *off, int device, void *stream);
+
+int pv_synth_fill_device(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t key_mod,
+                         uint32_t n_nodes, const uint64_t *off, uint8_t *blob, uint8_t *seeds, uint8_t *pk,
+                         uint8_t *sig, uint8_t *tamper, uint32_t *sender, int device, void *stream);
+
+/* FIXED-mode convenience (C2): layout + fill in one call; blob holds n*mlen + 16. */
 int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen, uint64_t *off,
                     uint8_t *blob, uint8_t *seeds, uint8_t *pk, uint8_t *sig, uint8_t *tamper, int device,
                     void *stream);

@@ -74,6 +74,7 @@ struct Device {
   DevBuf<uint64_t> off, bitmap, batch_off;
   DevBuf<uint32_t> sender, votes;
   DevBuf<uint8_t> reached;
+  DevBuf<uint64_t> scan;      // block sums of the device prefix scan
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -123,7 +124,7 @@ void release_device(Device& d) {
   d.btab.release(); d.scratch.release(); d.h.release(); d.pre.release();
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.bitmap.release(); d.batch_off.release();
-  d.sender.release(); d.votes.release(); d.reached.release();
+  d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -380,23 +381,57 @@ int pv_sign_batch(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t*
   return PV_OK;
 }
 
-int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen, uint64_t* off,
-                    uint8_t* blob, uint8_t* seeds, uint8_t* pk, uint8_t* sig, uint8_t* tamper, int device,
-                    void* stream) {
+int pv_synth_layout_device(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t mlen_min,
+                           uint32_t mlen_max, uint32_t n_nodes, uint64_t* off, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (!off) return fail(PV_EINVAL, "null device buffer");
+  if (mode > PV_SYNTH_COMMIT) return fail(PV_EINVAL, "unknown synth mode %u", mode);
+  if (mode == PV_SYNTH_RANGE && mlen_max < mlen_min) return fail(PV_EINVAL, "mlen_max < mlen_min");
+  if (mode == PV_SYNTH_COMMIT && (n_nodes == 0 || n_nodes > 1024))
+    return fail(PV_EINVAL, "n_nodes must be in 1..1024");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(d->scan.ensure(pv::scan_sums_words(n + 1)));
+  HIP_OK(pv::launch_synth_layout(cfg, mode, first, n, mlen_min, mlen_max, n_nodes, off, d->scan.p, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_synth_fill_device(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t key_mod,
+                         uint32_t n_nodes, const uint64_t* off, uint8_t* blob, uint8_t* seeds, uint8_t* pk,
+                         uint8_t* sig, uint8_t* tamper, uint32_t* sender, int device, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceGuard dg;
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (!off || !blob || !seeds || !pk || !sig || !tamper) return fail(PV_EINVAL, "null device buffer");
+  if (mode > PV_SYNTH_COMMIT) return fail(PV_EINVAL, "unknown synth mode %u", mode);
+  if (mode == PV_SYNTH_COMMIT && (n_nodes == 0 || n_nodes > 1024))
+    return fail(PV_EINVAL, "n_nodes must be in 1..1024");
   HIP_OK(hipSetDevice(device));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
-  HIP_OK(pv::launch_synth(cfg, first, n, key_mod, mlen, 0, 0, off, seeds, tamper, s));
-  HIP_OK(pv::launch_synth_fill(cfg, first, n, off, blob, s));
-  HIP_OK(hipMemsetAsync(blob + n * (uint64_t)mlen, 0, 16, s));
+  uint64_t total = 0;
+  HIP_OK(hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  HIP_OK(pv::launch_synth(cfg, mode, first, n, key_mod, n_nodes, seeds, tamper, sender, s));
+  HIP_OK(pv::launch_synth_fill(cfg, mode, first, n, n_nodes, off, blob, s));
+  HIP_OK(hipMemsetAsync(blob + total, 0, 16, s));
   HIP_OK(pv::launch_sign(seeds, blob, off, n, d->btab.p, pk, sig, s));
   HIP_OK(pv::launch_tamper(first, n, tamper, off, blob, sig, s));
   HIP_OK(hipStreamSynchronize(s));
   return PV_OK;
+}
+
+int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen, uint64_t* off,
+                    uint8_t* blob, uint8_t* seeds, uint8_t* pk, uint8_t* sig, uint8_t* tamper, int device,
+                    void* stream) {
+  int rc = pv_synth_layout_device(cfg, PV_SYNTH_FIXED, first, n, mlen, mlen, 0, off, device, stream);
+  if (rc) return rc;
+  return pv_synth_fill_device(cfg, PV_SYNTH_FIXED, first, n, key_mod, 0, off, blob, seeds, pk, sig, tamper, nullptr,
+                              device, stream);
 }
 
 }  // extern "C"

@@ -45,12 +45,18 @@ hipError_t launch_tally(const uint8_t* verdict, const uint32_t* sender, const ui
                         uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t* votes,
                         uint8_t* reached, hipStream_t s);
 
-// deterministic synthetic workload; see plenum_gpu/synth.py
-hipError_t launch_synth(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen_fixed,
-                        uint32_t mlen_min, uint32_t mlen_max, uint64_t* off_out, uint8_t* seeds_out,
-                        uint8_t* tamper_out, hipStream_t s);
-hipError_t launch_synth_fill(uint32_t cfg, uint64_t first, uint64_t n, const uint64_t* off, uint8_t* blob,
-                             hipStream_t s);
+// deterministic synthetic workload; spec in plenum_gpu/synth.py.
+// mode 0 FIXED (len = mlen_min), 1 RANGE (len uniform in [mlen_min, mlen_max]),
+// 2 COMMIT (C3 3PC batches of n_nodes votes).
+// off (n+1) <- exclusive prefix sum of message lengths; sums = scan_sums_words(n+1) words
+uint64_t scan_sums_words(uint64_t m);
+hipError_t launch_exclusive_scan(uint64_t* x, uint64_t m, uint64_t* sums, hipStream_t s);
+hipError_t launch_synth_layout(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t mlen_min,
+                               uint32_t mlen_max, uint32_t n_nodes, uint64_t* off, uint64_t* sums, hipStream_t s);
+hipError_t launch_synth(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t n_nodes,
+                        uint8_t* seeds_out, uint8_t* tamper_out, uint32_t* sender_out, hipStream_t s);
+hipError_t launch_synth_fill(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t n_nodes,
+                             const uint64_t* off, uint8_t* blob, hipStream_t s);
 hipError_t launch_tamper(uint64_t first, uint64_t n, const uint8_t* tamper, const uint64_t* off, uint8_t* blob,
                          uint8_t* sig, hipStream_t s);
 

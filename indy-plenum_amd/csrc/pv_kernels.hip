@@ -178,34 +178,210 @@ hipError_t launch_tally(const uint8_t* verdict, const uint32_t* sender, const ui
 }
 
 // ------------------------------------------------------- synthetic workload
-__global__ void k_synth(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen,
-                        uint64_t* __restrict__ off_out, uint8_t* __restrict__ seeds_out,
-                        uint8_t* __restrict__ tamper_out) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j > n) return;
-  off_out[j] = j * (uint64_t)mlen;
-  if (j == n) return;
-  const uint64_t i = first + j;
-  uint32_t w[16], d[16];
-  int nb = put_tag(w, "plenum-gpu/key", 14, cfg, key_mod ? i % key_mod : i, false, 0);
-  sha512_short(d, w, nb);
-  store8(seeds_out + 32 * j, d);
-  nb = put_tag(w, "plenum-gpu/tamper", 17, cfg, i, false, 0);
-  sha512_short(d, w, nb);
-  tamper_out[j] = d[0] < 214748365u ? 1 : 0;
+// Deterministic generator, spec in plenum_gpu/synth.py.
+// Three layouts: FIXED (C2: every M mlen bytes), RANGE (C4: len uniform in
+// [mlen_min, mlen_max] by hash), COMMIT (C3: 3PC batches of n_nodes COMMIT
+// votes, M = serialize_msg_for_signing(COMMIT) of the batch).
+
+// decimal digits of v >= 1
+PV_HD uint32_t ndigits(uint64_t v) {
+  uint32_t d = 1;
+  while (v >= 10) { v /= 10; ++d; }
+  return d;
 }
 
-__global__ void k_synth_fill(uint32_t cfg, uint64_t first, uint64_t n, const uint64_t* __restrict__ off,
-                             uint8_t* __restrict__ blob) {
+// per-batch COMMIT parameters: bad run start r, bad count k, duplicate slot/sender
+struct C3Batch { uint32_t r, k, dup_on, victim, dup; };
+
+PV_HD C3Batch c3_batch(uint64_t b, uint32_t n_nodes) {
+  // k_b from SHA-512("plenum-gpu/k" || u64le(b)) (no cfg byte: synth.c3_invalid_count)
+  uint32_t w[16], d[16];
+  const char* tag = "plenum-gpu/k";
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = 0;
+  for (int k = 0; k < 12; ++k) w[k >> 2] |= (uint32_t)(uint8_t)tag[k] << (8 * (k & 3));
+  for (int k = 0; k < 8; ++k) w[(12 + k) >> 2] |= (uint32_t)(uint8_t)(b >> (8 * k)) << (8 * ((12 + k) & 3));
+  int nb = 20;
+  sha512_short(d, w, nb);
+  C3Batch c;
+  c.k = (d[0] & 0xffu) % 13u;
+  nb = put_tag(w, "plenum-gpu/c3", 13, 3, b, false, 0);
+  sha512_short(d, w, nb);
+  const uint32_t b0 = d[0] & 0xffu, b1 = (d[0] >> 8) & 0xffu, b2 = (d[0] >> 16) & 0xffu;
+  const uint32_t b3 = d[0] >> 24, b4 = d[1] & 0xffu;
+  c.r = b0 % n_nodes;
+  c.dup_on = ((b1 | (b2 << 8)) < 655u && n_nodes > 1) ? 1u : 0u;
+  c.victim = b3 % n_nodes;
+  c.dup = n_nodes > 1 ? (c.victim + 1u + b4 % (n_nodes - 1u)) % n_nodes : 0u;
+  return c;
+}
+
+PV_HD uint32_t synth_len(uint32_t cfg, uint32_t mode, uint64_t i, uint32_t mlen_min, uint32_t mlen_max,
+                         uint32_t n_nodes) {
+  if (mode == 0) return mlen_min;
+  if (mode == 2) return 36u + ndigits(i / n_nodes + 1);  // "instId:0|op:COMMIT|ppSeqNo:" <n> "|viewNo:0"
+  uint32_t w[16], d[16];
+  const int nb = put_tag(w, "plenum-gpu/len", 14, cfg, i, false, 0);
+  sha512_short(d, w, nb);
+  return mlen_min + d[0] % (mlen_max - mlen_min + 1u);
+}
+
+// lens[j] = len(M_{first+j}), j < n
+__global__ void k_synth_len(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t mlen_min,
+                            uint32_t mlen_max, uint32_t n_nodes, uint64_t* __restrict__ lens) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) lens[j] = synth_len(cfg, mode, first + j, mlen_min, mlen_max, n_nodes);
+}
+
+// Exclusive prefix sum in place over x[0..n] (x[n] becomes the total):
+// SCAN_ITEMS per thread, block sums, one-block scan of block sums, add back.
+constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 8, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+__device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t sh[SCAN_BLOCK];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < SCAN_BLOCK; o <<= 1) {
+    const uint64_t t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  const uint64_t incl = sh[threadIdx.x];
+  *total = sh[SCAN_BLOCK - 1];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tiles(uint64_t* __restrict__ x, uint64_t m,
+                                                           uint64_t* __restrict__ sums) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  uint64_t v[SCAN_ITEMS], run = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    v[k] = base + k < m ? x[base + k] : 0;
+    const uint64_t t = v[k];
+    v[k] = run;
+    run += t;
+  }
+  uint64_t total;
+  const uint64_t pre = block_exclusive_scan(run, &total);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k)
+    if (base + k < m) x[base + k] = v[k] + pre;
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(uint64_t* __restrict__ sums, uint64_t nt) {
+  uint64_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nt; b0 += SCAN_BLOCK) {
+    const uint64_t j = b0 + threadIdx.x;
+    const uint64_t v = j < nt ? sums[j] : 0;
+    uint64_t total;
+    const uint64_t pre = block_exclusive_scan(v, &total);
+    if (j < nt) sums[j] = carry + pre;
+    carry += total;
+  }
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint64_t* __restrict__ x, uint64_t m,
+                                                         const uint64_t* __restrict__ sums) {
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  const uint64_t add = sums[blockIdx.x];
+  for (int k = threadIdx.x; k < SCAN_TILE; k += SCAN_BLOCK)
+    if (base + k < m) x[base + k] += add;
+}
+
+hipError_t launch_exclusive_scan(uint64_t* x, uint64_t m, uint64_t* sums, hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  const uint64_t tiles = (m + SCAN_TILE - 1) / SCAN_TILE;
+  hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)tiles), dim3(SCAN_BLOCK), 0, s, x, m, sums);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(SCAN_BLOCK), 0, s, sums, tiles);
+  hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)tiles), dim3(SCAN_BLOCK), 0, s, x, m, sums);
+  return hipGetLastError();
+}
+
+uint64_t scan_sums_words(uint64_t m) { return (m + SCAN_TILE - 1) / SCAN_TILE + 1; }
+
+hipError_t launch_synth_layout(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t mlen_min,
+                               uint32_t mlen_max, uint32_t n_nodes, uint64_t* off, uint64_t* sums, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(off + n, 0, 8, s);
+  if (e != hipSuccess) return e;
+  if (n) {
+    hipLaunchKernelGGL(k_synth_len, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, cfg, mode, first, n,
+                       mlen_min, mlen_max, n_nodes, off);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return launch_exclusive_scan(off, n + 1, sums, s);
+}
+
+// seeds, tamper flags and (COMMIT) senders for signature first + j
+__global__ void k_synth(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t n_nodes,
+                        uint8_t* __restrict__ seeds_out, uint8_t* __restrict__ tamper_out,
+                        uint32_t* __restrict__ sender_out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t i = first + j;
+  uint32_t w[16], d[16];
+  uint64_t key;
+  uint8_t bad;
+  if (mode == 2) {
+    const uint64_t b = i / n_nodes;
+    const uint32_t slot = (uint32_t)(i % n_nodes);
+    const C3Batch c = c3_batch(b, n_nodes);
+    const uint32_t snd = (c.dup_on && slot == c.victim) ? c.dup : slot;
+    key = snd;
+    bad = ((slot + n_nodes - c.r) % n_nodes) < c.k ? 1 : 0;
+    if (sender_out) sender_out[j] = snd;
+  } else {
+    key = key_mod ? i % key_mod : i;
+    const int nb = put_tag(w, "plenum-gpu/tamper", 17, cfg, i, false, 0);
+    sha512_short(d, w, nb);
+    bad = d[0] < 214748365u ? 1 : 0;
+    if (sender_out) sender_out[j] = 0;
+  }
+  const int nb = put_tag(w, "plenum-gpu/key", 14, cfg, key, false, 0);
+  sha512_short(d, w, nb);
+  store8(seeds_out + 32 * j, d);
+  tamper_out[j] = bad;
+}
+
+// message bytes of signature first + j at blob[off[j] - off[0] ...]
+__global__ void k_synth_fill(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t n_nodes,
+                             const uint64_t* __restrict__ off, uint8_t* __restrict__ blob) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint64_t i = first + j;
   const uint64_t o = off[j], len = off[j + 1] - o;
+  if (mode == 2) {
+    const char* head = "instId:0|op:COMMIT|ppSeqNo:";
+    const char* tail = "|viewNo:0";
+    uint64_t q = 0;
+    for (int k = 0; k < 27; ++k) blob[o + q++] = (uint8_t)head[k];
+    const uint64_t v = i / n_nodes + 1;
+    const uint32_t nd = ndigits(v);
+    uint64_t t = v;
+    for (int k = (int)nd - 1; k >= 0; --k) {
+      blob[o + q + k] = (uint8_t)('0' + t % 10);
+      t /= 10;
+    }
+    q += nd;
+    for (int k = 0; k < 9; ++k) blob[o + q++] = (uint8_t)tail[k];
+    return;
+  }
   uint32_t w[16], d[16];
   for (uint64_t c = 0; c * 64 < len; ++c) {
     const int nb = put_tag(w, "plenum-gpu/msg", 14, cfg, i, true, c);
     sha512_short(d, w, nb);
-    for (int k = 0; k < 64 && c * 64 + k < len; ++k) blob[o + c * 64 + k] = (uint8_t)(d[k >> 2] >> (8 * (k & 3)));
+    const uint64_t lim = len - c * 64 < 64 ? len - c * 64 : 64;
+    if (lim == 64 && ((o + c * 64) & 3) == 0) {
+      uint32_t* q = reinterpret_cast<uint32_t*>(blob + o + c * 64);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) q[k] = d[k];
+    } else {
+      for (uint64_t k = 0; k < lim; ++k) blob[o + c * 64 + k] = (uint8_t)(d[k >> 2] >> (8 * (k & 3)));
+    }
   }
 }
 
@@ -222,19 +398,19 @@ __global__ void k_tamper(uint64_t first, uint64_t n, const uint8_t* __restrict__
   else sig[64 * j + 32 + (i / 3) % 16] ^= bit;
 }
 
-hipError_t launch_synth(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t mlen_fixed, uint32_t,
-                        uint32_t, uint64_t* off_out, uint8_t* seeds_out, uint8_t* tamper_out, hipStream_t s) {
-  const uint64_t blocks = (n + 1 + 255) / 256;
-  hipLaunchKernelGGL(k_synth, dim3((uint32_t)blocks), dim3(256), 0, s, cfg, first, n, key_mod, mlen_fixed, off_out,
-                     seeds_out, tamper_out);
+hipError_t launch_synth(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t key_mod, uint32_t n_nodes,
+                        uint8_t* seeds_out, uint8_t* tamper_out, uint32_t* sender_out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_synth, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, cfg, mode, first, n, key_mod,
+                     n_nodes, seeds_out, tamper_out, sender_out);
   return hipGetLastError();
 }
 
-hipError_t launch_synth_fill(uint32_t cfg, uint64_t first, uint64_t n, const uint64_t* off, uint8_t* blob,
-                             hipStream_t s) {
+hipError_t launch_synth_fill(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n, uint32_t n_nodes,
+                             const uint64_t* off, uint8_t* blob, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(k_synth_fill, dim3((uint32_t)blocks), dim3(256), 0, s, cfg, first, n, off, blob);
+  hipLaunchKernelGGL(k_synth_fill, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, cfg, mode, first, n, n_nodes,
+                     off, blob);
   return hipGetLastError();
 }
 

@@ -35,6 +35,12 @@ SIGNATURES = [
     ('pv_synth_device', ctypes.c_int,
      [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp,
       _vp, ctypes.c_int, _vp]),
+    ('pv_synth_layout_device', ctypes.c_int,
+     [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_uint32, _vp, ctypes.c_int, _vp]),
+    ('pv_synth_fill_device', ctypes.c_int,
+     [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp,
+      _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
     ('pv_time_verify_device', ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int,
       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),

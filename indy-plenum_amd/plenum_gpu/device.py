@@ -20,26 +20,38 @@ def _stream(device):
 
 
 class SyntheticBatch:
-    """A signed synthetic batch resident in HBM (SoA: pk, sig, blob+off)."""
+    """A signed synthetic batch resident in HBM (SoA: pk, sig, blob+off).
 
-    def __init__(self, device, n, mlen, cfg=2, first=0, key_mod=0):
+    mode: synth.FIXED (C2, len = mlen), synth.RANGE (C4, len uniform in
+    [mlen, mlen_max]), synth.COMMIT (C3: n signatures = n / n_nodes 3PC
+    batches of COMMIT votes; `sender` holds each vote's node index)."""
+
+    def __init__(self, device, n, mlen, cfg=2, first=0, key_mod=0, mode=0, mlen_max=None, n_nodes=25):
         self.device = torch.device('cuda', device) if isinstance(device, int) else device
         nat.ensure_init(1 << self.device.index)
         dev = self.device
-        self.n, self.mlen, self.cfg, self.first = n, mlen, cfg, first
+        self.n, self.mlen, self.cfg, self.first, self.mode = n, mlen, cfg, first, mode
+        self.n_nodes = n_nodes
+        mlen_max = mlen if mlen_max is None else mlen_max
         u8 = dict(dtype=torch.uint8, device=dev)
+        lib = nat.load()
         self.off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        self.blob = torch.empty(n * mlen + 16, **u8)
+        nat._check('pv_synth_layout_device',
+                   lib.pv_synth_layout_device(cfg, mode, first, n, mlen, mlen_max, n_nodes, _p(self.off), dev.index,
+                                              _stream(dev)))
+        self.blob_bytes = int(self.off[n].item())
+        self.blob = torch.empty(self.blob_bytes + 16, **u8)
         self.seeds = torch.empty((n, 32), **u8)
         self.pk = torch.empty((n, 32), **u8)
         self.sig = torch.empty((n, 64), **u8)
         self.tamper = torch.empty(n, **u8)
+        self.sender = torch.empty(n, dtype=torch.int32, device=dev)
         self.verdict = torch.empty(n, **u8)
         self.bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
-        lib = nat.load()
-        nat._check('pv_synth_device', lib.pv_synth_device(cfg, first, n, key_mod, mlen, _p(self.off), _p(self.blob),
-                                                          _p(self.seeds), _p(self.pk), _p(self.sig), _p(self.tamper),
-                                                          dev.index, _stream(dev)))
+        nat._check('pv_synth_fill_device',
+                   lib.pv_synth_fill_device(cfg, mode, first, n, key_mod, n_nodes, _p(self.off), _p(self.blob),
+                                            _p(self.seeds), _p(self.pk), _p(self.sig), _p(self.tamper),
+                                            _p(self.sender), dev.index, _stream(dev)))
 
     def verify(self):
         """One pass of the hot path over the batch (hash + curve kernels)."""

@@ -1,4 +1,4 @@
-"""Deterministic synthetic workload (SURVEY.md §8(d), configs C2/C3).
+"""Deterministic synthetic workload (SURVEY.md §8(d), configs C2/C3/C4).
 
 Host restatement of the device generator (k_synth / k_synth_fill / k_tamper in
 csrc/pv_kernels.hip) so tests can check the device output byte for byte on
@@ -12,6 +12,18 @@ small index ranges.  All hashes are SHA-512 over a single block:
     tamper kind (i mod 3): 0 flip bit (i mod 8) of M byte (i/3) mod len(M)
                            1 flip bit (i mod 8) of R byte (i/3) mod 32
                            2 flip bit (i mod 8) of S byte (i/3) mod 16
+
+Layouts (csrc/pv_kernels.hip k_synth_len / k_synth / k_synth_fill):
+    FIXED  (C2)  len(M_i) = mlen
+    RANGE  (C4)  len(M_i) = lo + u32le(SHA-512("plenum-gpu/len" || cfg || u64le(i))[0:4]) mod (hi - lo + 1)
+    COMMIT (C3)  signature i = the COMMIT vote in slot s = i mod n of 3PC batch b = i div n:
+                 M = "instId:0|op:COMMIT|ppSeqNo:<b+1>|viewNo:0"
+                 k_b  = SHA-512("plenum-gpu/k" || u64le(b))[0] mod 13    invalid votes in the batch
+                 d    = SHA-512("plenum-gpu/c3" || 3 || u64le(b))
+                 r_b  = d[0] mod n                                       first invalid slot (a run of k_b, cyclic)
+                 dup  = u16le(d[1:3]) < 655 (~1 %): slot victim = d[3] mod n carries node
+                        (victim + 1 + d[4] mod (n-1)) mod n's vote instead of its own
+                 sender(b, s) signs with seed(3, sender); invalid slots get the tamper flip above.
 """
 import hashlib
 import struct
@@ -80,3 +92,65 @@ def commit_message(pp_seq_no):
 def c3_invalid_count(b):
     """k_b = SHA-512("plenum-gpu/k" || u64le(b))[0] mod 13."""
     return hashlib.sha512(b'plenum-gpu/k' + struct.pack('<Q', b)).digest()[0] % 13
+
+
+FIXED, RANGE, COMMIT = 0, 1, 2
+
+
+def msg_len(mode, cfg, i, lo, hi, n_nodes=25):
+    if mode == FIXED:
+        return lo
+    if mode == COMMIT:
+        return len(commit_message(i // n_nodes + 1))
+    return lo + struct.unpack('<I', _h(b'plenum-gpu/len', cfg, i)[:4])[0] % (hi - lo + 1)
+
+
+def c3_batch(b, n_nodes):
+    """(r_b, k_b, dup_on, victim, dup) of 3PC batch b."""
+    d = hashlib.sha512(b'plenum-gpu/c3' + bytes([3]) + struct.pack('<Q', b)).digest()
+    k = c3_invalid_count(b)
+    dup_on = n_nodes > 1 and (d[1] | (d[2] << 8)) < 655
+    victim = d[3] % n_nodes
+    dup = (victim + 1 + d[4] % (n_nodes - 1)) % n_nodes if n_nodes > 1 else 0
+    return d[0] % n_nodes, k, dup_on, victim, dup
+
+
+def c3_slots(b, n_nodes):
+    """senders (n_nodes,) and invalid flags (n_nodes,) of batch b."""
+    r, k, dup_on, victim, dup = c3_batch(b, n_nodes)
+    senders = np.arange(n_nodes, dtype=np.uint32)
+    if dup_on:
+        senders[victim] = dup
+    bad = ((np.arange(n_nodes) - r) % n_nodes) < k
+    return senders, bad
+
+
+def c3_expected(first_batch, n_batches, n_nodes, quorum):
+    """votes (distinct valid senders) and quorum-reached per batch, from the spec alone."""
+    votes = np.zeros(n_batches, np.uint32)
+    for j in range(n_batches):
+        senders, bad = c3_slots(first_batch + j, n_nodes)
+        votes[j] = len(set(senders[~bad].tolist()))
+    return votes, votes >= quorum
+
+
+def host_batch_ex(mode, cfg, first, n, lo, hi=None, key_mod=0, n_nodes=25):
+    """seeds, msgs, tamper, senders for signatures first..first+n-1 (unsigned) in any layout."""
+    hi = lo if hi is None else hi
+    seeds, msgs, tamper, senders = [], [], [], []
+    for j in range(n):
+        i = first + j
+        if mode == COMMIT:
+            b, s = divmod(i, n_nodes)
+            snd, bad = c3_slots(b, n_nodes)
+            senders.append(int(snd[s]))
+            tamper.append(bool(bad[s]))
+            seeds.append(seed(cfg, int(snd[s])))
+            msgs.append(commit_message(b + 1))
+        else:
+            senders.append(0)
+            tamper.append(tampered(cfg, i))
+            seeds.append(seed(cfg, i, key_mod))
+            msgs.append(message(cfg, i, msg_len(mode, cfg, i, lo, hi)))
+    return (np.frombuffer(b''.join(seeds), np.uint8).reshape(n, 32), msgs, np.array(tamper, dtype=bool),
+            np.array(senders, np.uint32))

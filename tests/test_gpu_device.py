@@ -70,3 +70,89 @@ def test_kernel_timer(torch_dev):
     b = SyntheticBatch(0, 65536, 256, cfg=2)
     th, tc = b.time_kernels(2)
     assert th > 0 and tc > 0 and tc > th
+
+
+def _check_against_spec(b, mode, cfg, first, n, lo, hi, key_mod=0, n_nodes=25):
+    from plenum_gpu import synth
+    seeds, msgs, tamper, senders = synth.host_batch_ex(mode, cfg, first, n, lo, hi, key_mod, n_nodes)
+    assert (b.seeds.cpu().numpy() == seeds).all()
+    assert (b.tamper.cpu().numpy().astype(bool) == tamper).all()
+    if mode == synth.COMMIT:
+        assert (b.sender.cpu().numpy().astype(np.uint32) == senders).all()
+    off = b.off.cpu().numpy().astype(np.uint64)
+    lens = np.array([len(m) for m in msgs], np.uint64)
+    assert (np.diff(off) == lens).all() and off[0] == 0
+    blob = b.blob.cpu().numpy()[:int(off[-1])]
+    pk2, sig2 = orc.sign_batch(seeds, np.frombuffer(b''.join(msgs), np.uint8), off)
+    pk = b.pk.cpu().numpy()
+    sig = b.sig.cpu().numpy()
+    assert (pk == pk2).all()
+    for j in range(n):
+        m2, s2 = msgs[j], sig2[j].tobytes()
+        if tamper[j]:
+            m2, s2 = synth.apply_tamper(first + j, m2, s2)
+        assert blob[int(off[j]):int(off[j + 1])].tobytes() == m2
+        assert sig[j].tobytes() == s2
+    v = b.verify().cpu().numpy().astype(bool)
+    assert (v == ~tamper).all()
+    assert (v == orc.verify_batch(pk, sig, blob, off)).all()
+
+
+def test_synth_range_matches_host_spec(torch_dev):
+    """C4 layout: ragged 128..4096-byte messages, key pool 2^20."""
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch
+    n, first = 700, (1 << 20) - 300
+    b = SyntheticBatch(0, n, 128, cfg=4, first=first, key_mod=1 << 20, mode=synth.RANGE, mlen_max=4096)
+    _check_against_spec(b, synth.RANGE, 4, first, n, 128, 4096, key_mod=1 << 20)
+    # the key pool wraps: signature i and i + 2^20 share a key
+    seeds = b.seeds.cpu().numpy()
+    assert (seeds[300] == np.frombuffer(synth.seed(4, 0), np.uint8)).all()
+
+
+def test_synth_commit_matches_host_spec(torch_dev):
+    """C3 layout: 25-node COMMIT votes of 3PC batches 9990..10029 (ppSeqNo digits change)."""
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch
+    n_nodes = 25
+    first = 9990 * n_nodes
+    b = SyntheticBatch(0, 40 * n_nodes, 0, cfg=3, first=first, mode=synth.COMMIT, n_nodes=n_nodes)
+    _check_against_spec(b, synth.COMMIT, 3, first, 40 * n_nodes, 0, 0, n_nodes=n_nodes)
+
+
+def test_c3_full_size_quorums(torch_dev):
+    """BASELINE configs[2]: 25-node pool (f = 8), 100k 3PC batches of COMMIT
+    votes: verify 2.5M signatures + n - f tally on one GPU; every quorum bit and
+    vote count equals the spec's voter-set count (synth.c3_expected)."""
+    import torch
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch, tally_device
+    from plenum_gpu.quorums import Quorums
+    n_nodes, nb = 25, 100_000
+    q = Quorums(n_nodes)
+    assert (q.f, q.commit.value, q.prepare.value) == (8, 17, 16)
+    b = SyntheticBatch(0, nb * n_nodes, 0, cfg=3, mode=synth.COMMIT, n_nodes=n_nodes)
+    v = b.verify()
+    assert (v.cpu().numpy().astype(bool) == ~b.tamper.cpu().numpy().astype(bool)).all()
+    dev = b.pk.device
+    boff = torch.arange(nb + 1, dtype=torch.int64, device=dev) * n_nodes
+    votes = torch.empty(nb, dtype=torch.int32, device=dev)
+    reached = torch.empty(nb, dtype=torch.uint8, device=dev)
+    tally_device(v, b.sender, boff, n_nodes, q.commit.value, votes, reached)
+    want_votes, want_reached = synth.c3_expected(0, nb, n_nodes, q.commit.value)
+    assert (votes.cpu().numpy() == want_votes.astype(np.int32)).all()
+    assert (reached.cpu().numpy().astype(bool) == want_reached).all()
+    assert 0.2 < want_reached.mean() < 0.9
+
+
+def test_c4_shape_properties(torch_dev):
+    """BASELINE configs[3] per-GPU shape at reduced count: ragged 128..4096-byte
+    messages, key pool 2^20, ~5 % tampered; verdict == not tampered."""
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch
+    n = 300_000
+    b = SyntheticBatch(0, n, 128, cfg=4, first=5 * n, key_mod=1 << 20, mode=synth.RANGE, mlen_max=4096)
+    v = b.verify().cpu().numpy().astype(bool)
+    tamper = b.tamper.cpu().numpy().astype(bool)
+    assert (v == ~tamper).all()
+    assert 0.045 < tamper.mean() < 0.055
