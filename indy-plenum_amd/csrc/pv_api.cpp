@@ -65,9 +65,11 @@ struct Device {
   hipStream_t stream = nullptr;
   int cu_count = 0;
   int curve_blocks = 0;
+  int hash_blocks = 0;
   DevBuf<uint32_t> btab;
   DevBuf<uint32_t> scratch;   // per-lane A tables for the persistent curve grid
-  DevBuf<uint32_t> h;         // 8 words per signature
+  DevBuf<uint32_t> h;         // SHA-512 digest, 16 words per signature
+  DevBuf<unsigned long long> counter;  // hash-kernel work queue
   DevBuf<uint8_t> pre;
   // staging for host-memory calls
   DevBuf<uint8_t> pk, sig, blob, verdict, tamper;
@@ -112,6 +114,11 @@ int init_device(Device& d) {
   if (per_cu > 4) per_cu = 4;
   d.curve_blocks = d.cu_count * per_cu;
   HIP_OK(d.scratch.ensure((size_t)d.curve_blocks * pv::CURVE_BLOCK * pv::ATAB_WORDS));
+  int hper = 0;
+  HIP_OK(pv::hash_occupancy(&hper));
+  if (hper < 1) hper = 1;
+  d.hash_blocks = d.cu_count * hper;
+  HIP_OK(d.counter.ensure(1));
   for (auto& e : d.ev) HIP_OK(hipEventCreate(&e));
   HIP_OK(hipStreamSynchronize(d.stream));
   return PV_OK;
@@ -121,7 +128,7 @@ void release_device(Device& d) {
   if (d.id < 0) return;
   (void)hipSetDevice(d.id);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
-  d.btab.release(); d.scratch.release(); d.h.release(); d.pre.release();
+  d.btab.release(); d.scratch.release(); d.h.release(); d.pre.release(); d.counter.release();
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.bitmap.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
@@ -137,7 +144,7 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
                    uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed, float* ms_hash,
                    float* ms_curve) {
   if (n == 0) return PV_OK;
-  HIP_OK(d.h.ensure(n * 8));
+  HIP_OK(d.h.ensure(n * 16));
   HIP_OK(d.pre.ensure(n));
   uint64_t* bm = bitmap;
   if (!bm) {
@@ -145,7 +152,7 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
     bm = d.bitmap.p;
   }
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
-  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.h.p, d.pre.p, s));
+  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.counter.p, d.h.p, d.pre.p, d.hash_blocks, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict, bm,
                           n, d.curve_blocks, s));

@@ -27,11 +27,15 @@ hipError_t launch_btable_init(uint32_t* btab, hipStream_t s);
 hipError_t curve_occupancy(int* blocks_per_cu);
 
 // pre[i] = 1 iff S canonical, R/A not small order, A canonical;
-// h[i] (8 words) = SHA-512(R||A||M) mod L
-hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
-                       uint64_t n, uint32_t* h, uint8_t* pre, hipStream_t s);
+// dig[i] (16 words) = SHA-512(R||A||M) when pre[i] (reduced mod L by the curve
+// kernel).  Persistent grid of `blocks` blocks; `counter` is an 8-byte device
+// word the launch resets (work queue).
+hipError_t hash_occupancy(int* blocks_per_cu);
+hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
+                       unsigned long long* counter, uint32_t* dig, uint8_t* pre, int blocks, hipStream_t s);
 
-// verdict[i] in {0,1}; bitmap[i/64] bit i%64 (bitmap must hold ceil(n/64) words)
+// verdict[i] in {0,1}; bitmap[i/64] bit i%64 (bitmap must hold ceil(n/64) words);
+// h = the hash kernel's digests (16 words per signature)
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s);

@@ -27,24 +27,77 @@ namespace pv {
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS, "table layout");
 
 // ------------------------------------------------------------- hash kernel
-__global__ __launch_bounds__(HASH_BLOCK, 2) void k_hash(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
-                                                      const uint8_t* __restrict__ blob,
-                                                      const uint64_t* __restrict__ off, uint64_t n,
-                                                      uint32_t* __restrict__ hout, uint8_t* __restrict__ pre) {
-  const uint64_t i = (uint64_t)blockIdx.x * HASH_BLOCK + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t o = off[i];
-  uint32_t h[8];
-  const bool ok = hash_one(h, pk + 32 * i, sig + 64 * i, blob + o, off[i + 1] - o);
-  pre[i] = ok ? 1 : 0;
-  store8(reinterpret_cast<uint8_t*>(hout + 8 * i), h);
+// Persistent lanes with per-lane refill: each lane runs ONE SHA-512
+// compression of its current message per loop trip and, when that message is
+// done, stores the digest and takes the next message index from a global
+// counter (one atomic per wavefront).  Ragged message lengths (C4: 2..33
+// blocks) then cost no SIMD divergence: a lane never waits for a longer
+// message in its wavefront, only the final drain is ragged.
+__device__ __forceinline__ uint64_t take_index(unsigned long long* counter) {
+  const uint64_t active = __ballot(1);
+  const int lane = (int)(threadIdx.x & 63u);
+  const int leader = __ffsll((unsigned long long)active) - 1;
+  const uint32_t rank = (uint32_t)__popcll(active & ((1ull << lane) - 1ull));
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(active));
+  base = __shfl(base, leader, 64);
+  return (uint64_t)base + rank;
+}
+
+#ifndef PV_HASH_WAVES
+#define PV_HASH_WAVES 2
+#endif
+__global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                                     const uint8_t* __restrict__ blob,
+                                                     const uint64_t* __restrict__ off, uint64_t n,
+                                                     unsigned long long* __restrict__ counter,
+                                                     uint32_t* __restrict__ dig, uint8_t* __restrict__ pre) {
+  uint64_t idx = take_index(counter);
+  uint64_t blk = 0, nblk = 0, mo = 0, ml = 0;
+  uint64_t hs[8];
+  while (true) {
+    // refill: skip messages that fail the pre-checks
+    while (blk == nblk && idx < n) {
+      const bool ok = precheck(pk + 32 * idx, sig + 64 * idx);
+      pre[idx] = ok ? 1 : 0;
+      if (ok) {
+        mo = off[idx];
+        ml = off[idx + 1] - mo;
+        nblk = hram_blocks(ml);
+        blk = 0;
+        sha512_init(hs);
+      } else {
+        idx = take_index(counter);
+      }
+    }
+    if (idx >= n) break;
+    uint64_t w[16];
+    hram_block(w, sig + 64 * idx, pk + 32 * idx, blob + mo, ml, blk, nblk);
+    sha512_compress(hs, w);
+    if (++blk == nblk) {
+      uint32_t d[16];
+      sha512_digest_words(d, hs);
+      uint32_t* o = dig + 16 * idx;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) o[k] = d[k];
+      idx = take_index(counter);
+    }
+  }
+}
+
+hipError_t hash_occupancy(int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_hash),
+                                                      HASH_BLOCK, 0);
 }
 
 hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
-                       uint32_t* h, uint8_t* pre, hipStream_t s) {
+                       unsigned long long* counter, uint32_t* dig, uint8_t* pre, int blocks, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t blocks = (n + HASH_BLOCK - 1) / HASH_BLOCK;
-  hipLaunchKernelGGL(k_hash, dim3((uint32_t)blocks), dim3(HASH_BLOCK), 0, s, pk, sig, blob, off, n, h, pre);
+  hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  const uint64_t need = (n + HASH_BLOCK - 1) / HASH_BLOCK;
+  const uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
+  hipLaunchKernelGGL(k_hash, dim3((uint32_t)b), dim3(HASH_BLOCK), 0, s, pk, sig, blob, off, n, counter, dig, pre);
   return hipGetLastError();
 }
 

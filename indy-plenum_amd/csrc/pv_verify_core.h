@@ -93,21 +93,90 @@ PV_HD void sha512_prefixed(uint32_t out[16], const uint32_t* pre, int pre_words6
 }
 
 // ------------------------------------------------------------------ hash
-// pre-checks + h = SHA-512(R||A||M) mod L.  Returns the pre-check verdict.
-PV_HD bool hash_one(uint32_t h[8], const uint8_t* pk, const uint8_t* sig, const uint8_t* m, uint64_t mlen) {
-  uint32_t ra[16], sw[8];
-  load8(ra, sig);
+// libsodium 1.0.18 pre-checks on (R, A, S)
+PV_HD bool precheck(const uint8_t* pk, const uint8_t* sig) {
+  uint32_t r[8], a[8], sw[8];
+  load8(r, sig);
   load8(sw, sig + 32);
-  load8(ra + 8, pk);
-  const bool ok = sc_is_canonical(sw) && !has_small_order(ra) && y_is_canonical(ra + 8) && !has_small_order(ra + 8);
+  load8(a, pk);
+  return sc_is_canonical(sw) && !has_small_order(r) && y_is_canonical(a) && !has_small_order(a);
+}
+
+// SHA-512 compressions of R || A || M
+PV_HD uint64_t hram_blocks(uint64_t mlen) { return (64 + mlen + 17 + 127) / 128; }
+
+PV_HD uint32_t funnel32(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+#endif
+}
+
+// 32 little-endian words = message bytes [q, q + 128) with SHA padding
+// applied: bytes past mlen are zero and byte mlen is 0x80.  One guarded
+// aligned load per word that holds a message byte, then a funnel shift: the
+// blob only needs the usual 16 readable bytes after the last message.
+PV_HD void msg_window(uint32_t x[32], const uint8_t* m, uint64_t mlen, uint64_t q) {
+  const int64_t rem = (int64_t)mlen - (int64_t)q;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(m) + q;
+  const uint32_t mis = (uint32_t)(base & 3u);
+  const uint32_t* wp = reinterpret_cast<const uint32_t*>(base - mis);
+  uint32_t y[33];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) h[k] = 0;
-  if (ok) {
-    uint32_t dig[16];
-    sha512_prefixed(dig, ra, 8, m, mlen);
-    sc_reduce64(h, dig);
+  for (int k = 0; k < 33; ++k) y[k] = (int64_t)(4 * k) - (int64_t)mis < rem ? wp[k] : 0u;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t v = funnel32(y[k + 1], y[k], 8u * mis);
+    const int64_t r = rem - 4 * k;
+    if (r < 4) {
+      const uint32_t keep = r <= 0 ? 0u : (1u << (8 * (uint32_t)r)) - 1u;
+      v = (v & keep) | ((r >= 0) ? (0x80u << (8 * (uint32_t)r)) : 0u);
+    }
+    x[k] = v;
   }
-  return ok;
+}
+
+// block `blk` of R || A || M as 16 big-endian 64-bit words (R, A read from
+// sig/pk on block 0; length words on the last block)
+PV_HD void hram_block(uint64_t w[16], const uint8_t* sig, const uint8_t* pk, const uint8_t* m, uint64_t mlen,
+                      uint64_t blk, uint64_t nblk) {
+  const bool first = blk == 0;
+  uint32_t x[32];
+  msg_window(x, m, mlen, first ? 0 : 128 * blk - 64);
+  if (first) {
+    uint32_t ra[16];
+    load8(ra, sig);
+    load8(ra + 8, pk);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      w[j] = be64_from_le32(ra[2 * j], ra[2 * j + 1]);
+      w[8 + j] = be64_from_le32(x[2 * j], x[2 * j + 1]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = be64_from_le32(x[2 * j], x[2 * j + 1]);
+  }
+  if (blk + 1 == nblk) {
+    w[14] = 0;
+    w[15] = (64 + mlen) * 8;
+  }
+}
+
+// pre-checks + digest = SHA-512(R||A||M) as 16 LE words (reduced mod L by the
+// curve stage).  Returns the pre-check verdict; the digest is only written
+// when it passes.
+PV_HD bool hash_one(uint32_t dig[16], const uint8_t* pk, const uint8_t* sig, const uint8_t* m, uint64_t mlen) {
+  if (!precheck(pk, sig)) return false;
+  uint64_t h[8], w[16];
+  sha512_init(h);
+  const uint64_t nb = hram_blocks(mlen);
+  for (uint64_t b = 0; b < nb; ++b) {
+    hram_block(w, sig, pk, m, mlen, b, nb);
+    sha512_compress(h, w);
+  }
+  sha512_digest_words(dig, h);
+  return true;
 }
 
 // ------------------------------------------------------------ table access
@@ -307,7 +376,7 @@ PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss
 // kernel).  Inputs are loaded right where they are consumed so that no
 // 32-byte value stays live across the whole verification (register budget of
 // the hot loop).  false = rejected before the final comparison.
-PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const uint32_t* hh_src, uint32_t* atab,
+PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const uint32_t* dig_src, uint32_t* atab,
                        const uint32_t* btab) {
   ge_p3 negA;
   {
@@ -317,7 +386,12 @@ PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const u
   }
   build_atab(atab, negA);
   uint32_t hh[8], S[8];
-  load8(hh, reinterpret_cast<const uint8_t*>(hh_src));
+  {
+    uint32_t dig[16];
+    load8(dig, reinterpret_cast<const uint8_t*>(dig_src));
+    load8(dig + 8, reinterpret_cast<const uint8_t*>(dig_src + 8));
+    sc_reduce64(hh, dig);  // h = SHA-512(R||A||M) mod L (App. C.2 step 5)
+  }
   load8(S, sig + 32);
   double_scalarmult(rp, hh, S, atab, btab);
   return true;
@@ -365,7 +439,7 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     const uint64_t i = i0 + (uint64_t)k * stride;
     ge_p2 rp;
     bool ok = false;
-    if (i < n && pre[i]) ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 8 * i, scratch, btab);
+    if (i < n && pre[i]) ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);
     if (!ok) {
       fe_0(rp.X);
       fe_0(rp.Y);

@@ -73,10 +73,10 @@ void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                      uint8_t* verdict) {
   ensure_btab();
   static uint32_t lane[LANE_WORDS];
-  uint32_t* h = (uint32_t*)calloc(n ? n * 8 : 8, sizeof(uint32_t));
+  uint32_t* h = (uint32_t*)calloc(n ? n * 16 : 16, sizeof(uint32_t));
   uint8_t* pre = (uint8_t*)calloc(n ? n : 1, 1);
   for (uint64_t i = 0; i < n; ++i)
-    pre[i] = hash_one(h + 8 * i, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+    pre[i] = hash_one(h + 16 * i, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
   for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
     const uint32_t okm = curve_group(pk, sig, h, pre, i0, 1, n, lane, g_btab);
     for (int k = 0; k < CURVE_K && i0 + k < n; ++k) verdict[i0 + k] = (okm >> k) & 1u;

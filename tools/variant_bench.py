@@ -27,14 +27,21 @@ def main():
     ap.add_argument('libs', nargs='+')
     ap.add_argument('--n', type=int, default=1_000_000)
     ap.add_argument('--rounds', type=int, default=5)
+    ap.add_argument('--mode', type=int, default=0, help='synth layout: 0 FIXED (C2), 1 RANGE (C4), 2 COMMIT (C3)')
+    ap.add_argument('--mlen', type=int, default=256)
+    ap.add_argument('--mlen-max', type=int, default=None)
+    ap.add_argument('--key-mod', type=int, default=0)
+    ap.add_argument('--cfg', type=int, default=2)
     a = ap.parse_args()
-    b = SyntheticBatch(0, a.n, 256)
+    b = SyntheticBatch(0, a.n, a.mlen, cfg=a.cfg, mode=a.mode, mlen_max=a.mlen_max, key_mod=a.key_mod)
     torch.cuda.synchronize()
     tamper = b.tamper.cpu().numpy().astype(bool)
     libs = []
     for path in a.libs:
         lib = ctypes.CDLL(os.path.abspath(path))
         for name, res, args in nat.SIGNATURES:
+            if not hasattr(lib, name):
+                continue
             getattr(lib, name).restype = res
             getattr(lib, name).argtypes = args
         assert lib.pv_init(1) == 0, lib.pv_last_error()
