@@ -44,6 +44,10 @@ CONFIGS = {
     'c3': dict(mode=synth.COMMIT, n=2_500_000, cfg=3, mlen=0, mlen_max=0, key_mod=0, n_nodes=25,
                workload='C3: 25-node pool (f=8), 100k 3PC batches of per-node COMMIT signatures per GPU, '
                         'verify + n-f quorum tally (BASELINE.json configs[2])'),
+    'c1': dict(mode=None, n=10_000, cfg=1, mlen=0, mlen_max=0, key_mod=0,
+               workload='C1: Plenum request authentication, CoreAuthNr.authenticate over 10k signed write requests '
+                        '(256-char payload, DidSigner abbreviated verkeys), batched through ReqAuthenticator-style '
+                        'authenticate_batch (BASELINE.json configs[0])'),
     'c4': dict(mode=synth.RANGE, n=8_000_000, cfg=4, mlen=128, mlen_max=4096, key_mod=1 << 20,
                workload='C4: 64M signatures over 8 GPUs = 8M per GPU, payloads uniform 128 B-4 KB, key pool 2^20, '
                         '~5% tampered, RCCL all-gather of verdict bitmaps (BASELINE.json configs[3])'),
@@ -127,6 +131,104 @@ def cpu_baseline(batch, workload, seconds=1.5, sample=8192):
                       'of the {} workload, host {}'.format(name, threads, seconds, rate1, sample, workload, cpu)}
 
 
+class _SodiumVerifyKey:
+    """libsodium 1.0.18 crypto_sign_open on the host: the native call under the
+    reference's VerifyKey.verify (stp_core/crypto/nacl_wrappers.py:86-108).
+    cpu_baseline only: the product has no CPU verify path."""
+    lib = None
+
+    def __init__(self, raw):
+        if _SodiumVerifyKey.lib is None:
+            _SodiumVerifyKey.lib = ctypes.CDLL('/opt/conda/lib/libsodium.so.23')
+            _SodiumVerifyKey.lib.sodium_init()
+        self.raw = bytes(raw)
+
+    def verify(self, sm):
+        m = ctypes.create_string_buffer(len(sm))
+        mlen = ctypes.c_ulonglong()
+        return _SodiumVerifyKey.lib.crypto_sign_open(m, ctypes.byref(mlen), sm, ctypes.c_ulonglong(len(sm)),
+                                                     self.raw) == 0
+
+
+def _sodium_did_verifier():
+    from plenum_gpu.base58 import b58decode
+    from plenum_gpu.verifier import DidVerifier
+
+    class SodiumDidVerifier(DidVerifier):
+        """DidVerifier (plenum/common/verifier.py:25-54) verifying on the host with libsodium."""
+        @DidVerifier.verkey.setter
+        def verkey(self, value):
+            self._verkey = value
+            raw = b58decode(value)
+            if len(raw) != 32:
+                raise ValueError('The key must be exactly 32 bytes long')
+            self._sk = _SodiumVerifyKey(raw)
+            self._vr = None
+
+        @property
+        def raw_verkey(self):
+            return None   # never served from the GPU prefetch cache
+
+        def verify(self, sig, msg):
+            return self._sk.verify(bytes(sig) + bytes(msg))
+    return SodiumDidVerifier
+
+
+def main_c1(args):
+    """C1: the Plenum request-authentication path end to end (host preprocessing
+    + one GPU verify per batch) vs the same per-request path on libsodium."""
+    from plenum_gpu.client_authn import CoreAuthNr
+    cfg = CONFIGS['c1']
+    n = args.n or cfg['n']
+    torch.cuda.set_device(0)
+    reqs, ids = synth.c1_requests(n)
+    authnr = CoreAuthNr(['buy'], [], [])
+    for idr, vk in ids:
+        authnr.addIdr(idr, vk)
+    want = [[idr] for idr, _ in ids]
+    for _ in range(args.warmup):
+        authnr.authenticate_batch(reqs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = authnr.authenticate_batch(reqs)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    mism = sum(1 for a, b in zip(out, want) if a != b)
+    value = n * args.steps / elapsed
+    res = {
+        'metric': METRIC, 'value': round(value, 1), 'unit': 'verifies/s', 'n_gpus': 1, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',
+        'data': 'synthetic signed requests (plenum_gpu/synth.py c1_requests), one signature per request',
+        'config': {'workload': cfg['workload'], 'name': 'c1', 'requests': n, 'host_threads': 1},
+        'verdict_mismatches': mism,
+        'roofline': None,
+        'note': 'host-bound: base58/serialization/key resolution per request on 1 thread (native _host module); '
+                'the GPU verify of the batch is a few percent of the step',
+        'cpu_baseline': None,
+    }
+    if not args.no_cpu_baseline:
+        sv = _sodium_did_verifier()
+        base = CoreAuthNr(['buy'], [], [])
+        base._verifier = lambda verifier, verkey, idr: verifier(verkey, identifier=idr)  # fresh key per call, as the reference
+        for idr, vk in ids:
+            base.addIdr(idr, vk)
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            r = reqs[done % n]
+            assert base.authenticate(r, verifier=sv) == [r['identifier']]
+            done += 1
+        rate = done / (time.perf_counter() - t0)
+        res['cpu_baseline'] = {
+            'value': round(rate, 1), 'unit': 'verifies/s', 'cores': 1, 'kind': 'port',
+            'sample': '{} requests (3 s) through the same CoreAuthNr.authenticate path one request at a time, '
+                      'verification by libsodium 1.0.18 crypto_sign_open on 1 host thread (the node verifies on its '
+                      'single Looper thread)'.format(done)}
+    print(json.dumps(res), flush=True)
+    return 0 if mism == 0 else 3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -136,6 +238,8 @@ def main():
     ap.add_argument('--n', type=int, default=None, help='signatures per GPU (default: the config\'s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
+    if args.config == 'c1':
+        return main_c1(args)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))

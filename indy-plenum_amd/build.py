@@ -44,6 +44,20 @@ def _run(cmd):
     return r.stdout + r.stderr
 
 
+def build_host(force=False):
+    """plenum_gpu/_host (CPython extension, g++): native base58 + signing serializer."""
+    import sysconfig
+    src = os.path.join(CSRC, 'pv_host.cpp')
+    out = os.path.join(HERE, 'plenum_gpu', '_host' + sysconfig.get_config_var('EXT_SUFFIX'))
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    tmp = out + '.tmp'
+    _run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-Wall', '-I' + sysconfig.get_paths()['include'], src,
+          '-o', tmp])
+    os.replace(tmp, out)
+    return out
+
+
 def build(force=False, verbose=False, defines=(), lib=None):
     """Compile the library; `defines`/`lib` build named variants for A/B timing."""
     os.makedirs(LIBDIR, exist_ok=True)
@@ -81,5 +95,7 @@ if __name__ == '__main__':
     ap.add_argument('-D', dest='defines', action='append', default=[], help='extra -D for a variant build')
     ap.add_argument('-o', dest='lib', default=None, help='output .so for a variant build')
     a = ap.parse_args()
+    if not a.lib:
+        print(build_host(force=a.force))
     print(build(force=a.force, verbose=a.verbose, defines=a.defines, lib=a.lib))
     sys.exit(0)

@@ -15,7 +15,7 @@ def _as_bytes(v):
     return bytes(v)
 
 
-def b58encode(v):
+def _py_b58encode(v):
     raw = _as_bytes(v)
     stripped = raw.lstrip(b'\0')
     zeros = len(raw) - len(stripped)
@@ -27,7 +27,7 @@ def b58encode(v):
     return b'1' * zeros + bytes(reversed(digits))
 
 
-def b58decode(v):
+def _py_b58decode(v):
     text = _as_bytes(v.rstrip())
     body = text.lstrip(b'1')
     zeros = len(text) - len(body)
@@ -39,3 +39,32 @@ def b58decode(v):
         num = num * 58 + d
     out = num.to_bytes((num.bit_length() + 7) // 8, 'big') if num else b''
     return b'\0' * zeros + out
+
+
+# Native implementations (csrc/pv_host.cpp); inputs the
+# restatement treats specially or rejects take the Python path above, so
+# results and exceptions are identical.
+try:
+    from . import _host
+    NATIVE = True
+except ImportError:  # not built yet: the restatement alone (host preprocessing, not the verify path)
+    _host = None
+    NATIVE = False
+
+
+def b58encode(v):
+    if _host is not None:
+        try:
+            return _host.b58encode(v)
+        except _host.Fallback:
+            pass
+    return _py_b58encode(v)
+
+
+def b58decode(v):
+    if _host is not None:
+        try:
+            return _host.b58decode(v)
+        except _host.Fallback:
+            pass
+    return _py_b58decode(v)

@@ -101,6 +101,24 @@ class ClientAuthNr:
 
 
 class NaclAuthNr(ClientAuthNr):
+    # key objects are pure functions of (verifier class, verkey, identifier):
+    # re-resolving the same key (base58 decodes, key checks) per request is
+    # skipped; construction errors are never cached, so they re-raise as in
+    # the reference
+    VERIFIER_CACHE_MAX = 1 << 16
+
+    def _verifier(self, verifier, verkey, idr):
+        cache = getattr(self, '_vr_cache', None)
+        if cache is None:
+            cache = self._vr_cache = {}
+        key = (verifier, verkey, idr)
+        vr = cache.get(key)
+        if vr is None:
+            vr = verifier(verkey, identifier=idr)
+            if len(cache) >= self.VERIFIER_CACHE_MAX:
+                cache.clear()
+            cache[key] = vr
+        return vr
 
     def _verdicts(self):
         cache = getattr(self, '_verdict_cache', None)
@@ -135,7 +153,7 @@ class NaclAuthNr(ClientAuthNr):
             verkey = self.getVerkey(idr, msg)
             if verkey is None:
                 raise CouldNotAuthenticate(idr)
-            vr = verifier(verkey, identifier=idr)
+            vr = self._verifier(verifier, verkey, idr)
             if self._check_one(vr, sig_decoded, ser):
                 accepted.append(idr)
                 if len(accepted) == threshold:
@@ -167,7 +185,7 @@ class NaclAuthNr(ClientAuthNr):
                 verkey = self.getVerkey(idr, msg)
                 if verkey is None:
                     continue
-                vr = verifier(verkey, identifier=idr)
+                vr = self._verifier(verifier, verkey, idr)
             except Exception:
                 continue
             raw = getattr(vr, 'raw_verkey', None)

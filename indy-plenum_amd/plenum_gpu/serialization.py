@@ -42,5 +42,16 @@ class SigningSerializer:
 signing_serializer = SigningSerializer()
 
 
+try:
+    from . import _host   # native serializer (csrc/pv_host.cpp)
+except ImportError:
+    _host = None
+
+
 def serialize_msg_for_signing(msg, topLevelKeysToIgnore=None):
+    if _host is not None:
+        try:
+            return _host.serialize(msg, topLevelKeysToIgnore)
+        except _host.Fallback:
+            pass  # unacceptable/special input: the restatement raises or handles it exactly
     return signing_serializer.serialize(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)

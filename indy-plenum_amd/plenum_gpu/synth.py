@@ -154,3 +154,32 @@ def host_batch_ex(mode, cfg, first, n, lo, hi=None, key_mod=0, n_nodes=25):
             msgs.append(message(cfg, i, msg_len(mode, cfg, i, lo, hi)))
     return (np.frombuffer(b''.join(seeds), np.uint8).reshape(n, 32), msgs, np.array(tamper, dtype=bool),
             np.array(senders, np.uint32))
+
+
+# ---------------------------------------------------------------- C1 requests
+def c1_identity(pk):
+    """DidSigner(seed) identity for raw key pk: (identifier, abbreviated verkey)
+    (plenum/common/signer_did.py: identifier = b58(vk[:16]), verkey = '~' + b58(vk[16:]))."""
+    from .base58 import b58encode
+    return b58encode(pk[:16]).decode(), '~' + b58encode(pk[16:]).decode()
+
+
+def c1_requests(n, first=0, cfg=1):
+    """BASELINE configs[0]: n signed write requests
+    {'identifier', 'reqId', 'operation': {'type': 'buy', 'data': 256 chars a-z}, 'protocolVersion': 2}
+    signed by DidSigner(seed_i) (GPU batch signer).  Returns (requests, [(identifier, verkey)])."""
+    from .base58 import b58encode
+    from .nacl_wrappers import sign_batch
+    from .serialization import serialize_msg_for_signing
+    seeds = [seed(cfg, first + j) for j in range(n)]
+    pk, _ = sign_batch(seeds, [b''] * n)
+    ids = [c1_identity(pk[j].tobytes()) for j in range(n)]
+    reqs = []
+    for j in range(n):
+        data = ''.join(chr(97 + b % 26) for b in message(cfg, first + j, 256))
+        reqs.append({'identifier': ids[j][0], 'reqId': first + j, 'operation': {'type': 'buy', 'data': data},
+                     'protocolVersion': 2})
+    _, sig = sign_batch(seeds, [serialize_msg_for_signing(r) for r in reqs])
+    for j in range(n):
+        reqs[j]['signature'] = b58encode(sig[j].tobytes()).decode()
+    return reqs, ids

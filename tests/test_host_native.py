@@ -1,0 +1,80 @@
+"""Native host preprocessing (csrc/pv_host.cpp -> plenum_gpu._host, SURVEY.md
+§8 f2) is byte-identical to the base58 / signing-serializer restatements,
+including every rejected input (same exception type and text)."""
+import random
+
+import pytest
+
+from plenum_gpu import base58, serialization
+
+
+def _outcome(fn, *a):
+    try:
+        return ('ok', fn(*a))
+    except Exception as ex:  # noqa: BLE001 - comparing exact exceptions
+        return ('err', type(ex), str(ex))
+
+
+def test_native_module_loaded():
+    import sys
+    sys.path.insert(0, serialization.__file__.rsplit('/', 2)[0])
+    import build
+    build.build_host()
+    import importlib
+    importlib.reload(base58)
+    importlib.reload(serialization)
+    assert base58.NATIVE and serialization._host is not None
+
+
+def test_base58_roundtrip_random():
+    rng = random.Random(7)
+    alpha = base58.ALPHABET.decode()
+    for n in range(0, 130):
+        for _ in range(20):
+            raw = bytes(rng.choice([0, 0, 1, 255, rng.randrange(256)]) for _ in range(n))
+            e = base58.b58encode(raw)
+            assert e == base58._py_b58encode(raw)
+            assert base58.b58decode(e) == raw == base58.b58decode(e.decode())
+            s = ''.join(rng.choice(alpha) for _ in range(n))
+            assert base58.b58decode(s) == base58._py_b58decode(s)
+
+
+@pytest.mark.parametrize('v', ['0abc', 'abcI', 'abcl', 'é', 'ab c', b'abc\x1f', 'abc\x1c', 'zz\n\t ', b'11', '',
+                               3, memoryview(b'abc'), bytearray(b'3yZe7d'), None, ['a']])
+def test_base58_decode_edges_identical(v):
+    assert _outcome(base58.b58decode, v) == _outcome(base58._py_b58decode, v)
+
+
+@pytest.mark.parametrize('v', [b'', b'\0\0', 'abc', 'é', 3, memoryview(b'\0ab'), bytearray(b'\0\1'), [1, 2], None])
+def test_base58_encode_edges_identical(v):
+    assert _outcome(base58.b58encode, v) == _outcome(base58._py_b58encode, v)
+
+
+class _IntSub(int):
+    def __str__(self):
+        return 'sub'
+
+
+class _DictSub(dict):
+    pass
+
+
+CASES = [
+    {'a': 1, 'b': [1, 2, {'x': None, 'y': 1.5}], 'c': 'é€😀', 'd': True, 'e': False},
+    {'z': {}, 'y': [], 'x': ''}, 'abc', 5, -7, 1e300, float('nan'), None, [1, 'a', None, [2, [3]]],
+    {'signature': 'x', 'k': 1, 'signatures': {'a': 'b'}}, {1: 'a', 2: 'b', -1: 'c'}, {'a': (1, 2)},
+    {'a': object()}, {1: 'a', 'b': 2}, {'a': {'b': {'c': [[], [None], 'q']}}}, {'a': _IntSub(3)},
+    _DictSub(b=1, a=2), {'a': _DictSub(x=1)}, {'a': '\ud800'}, {'a': b'bytes'}, {'a': {1, 2}},
+    {'operation': {'type': 'buy', 'data': 'x' * 300}, 'reqId': 12, 'identifier': 'Id', 'protocolVersion': 2},
+]
+
+
+@pytest.mark.parametrize('case', range(len(CASES)))
+@pytest.mark.parametrize('ignore', [None, [], ['signature'], {'k', 'signatures'}, ('a',)])
+def test_serializer_identical(case, ignore):
+    obj = CASES[case]
+    want = _outcome(serialization.signing_serializer.serialize, obj, 0, None, ignore)
+    got = _outcome(serialization.serialize_msg_for_signing, obj, ignore)
+    if want[0] == 'ok' and isinstance(obj, float) and obj != obj:
+        assert got == want
+    assert got == want
