@@ -62,6 +62,11 @@ CONFIGS = {
 W_MUL_PER_VERIFY = 1581.5
 W_SQ_PER_VERIFY = 1326.5
 W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
+# keyed batches (prepared keys): the curve kernel skips decompression and the
+# table build; those run once per distinct key in the key-preparation kernel
+W_MUL_KEYED, W_SQ_KEYED = 1498.0, 1071.5
+W_MUL_KEYPREP, W_SQ_KEYPREP = 83.5, 255.0
+W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
 # v_mad_u64_u32 issue ceiling of one MI355X measured by tools/ubench/mad_peak.hip
 # (profiles/r01_mad_peak.json, best over 1..8 waves/SIMD): lane-ops/s, whole chip.
 P_MAD_PER_S = 3.3896e13
@@ -237,6 +242,8 @@ def main():
     ap.add_argument('--config', choices=sorted(CONFIGS), default='c2', help='workload (default c2, the headline)')
     ap.add_argument('--n', type=int, default=None, help='signatures per GPU (default: the config\'s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-key-cache', action='store_true',
+                    help='c3/c4: re-decompress every key per signature instead of preparing each distinct key once')
     args = ap.parse_args()
     if args.config == 'c1':
         return main_c1(args)
@@ -256,6 +263,7 @@ def main():
         n -= n % n_nodes
     batch = SyntheticBatch(local, n, cfg['mlen'], cfg=cfg['cfg'], first=rank * n, key_mod=cfg['key_mod'],
                            mode=cfg['mode'], mlen_max=cfg['mlen_max'], n_nodes=n_nodes)
+    key_cache = batch.use_key_cache(not args.no_key_cache)   # keys repeat in c3 (node keys) and c4 (key pool)
     torch.cuda.synchronize()
     gathered = torch.zeros(world * batch.bitmap.numel(), dtype=torch.int64, device=dev) if world > 1 else None
     tally = None
@@ -314,7 +322,8 @@ def main():
 
     # kernel-level timing (HIP events on the launch stream) for the roofline
     ms_hash, ms_curve = batch.time_kernels(3)
-    achieved = W_MAD_PER_VERIFY * n / (ms_curve * 1e-3)
+    w_mad = W_MAD_KEYED if key_cache else W_MAD_PER_VERIFY
+    achieved = w_mad * n / (ms_curve * 1e-3)
     peak = _mad_peak()
 
     total = world * n * args.steps
@@ -327,7 +336,9 @@ def main():
         'config': {'workload': cfg['workload'], 'name': args.config,
                    'signatures_per_gpu': n, 'msg_bytes': [cfg['mlen'], cfg['mlen_max']] if cfg['mlen'] != cfg['mlen_max']
                    else cfg['mlen'], 'mean_msg_bytes': round(batch.blob_bytes / max(1, n), 1),
-                   'key_pool': cfg['key_mod'] or 'distinct', 'tampered': int(tamper.sum()),
+                   'key_pool': cfg['key_mod'] or ('node keys' if cfg['mode'] == synth.COMMIT else 'distinct'),
+                   'key_cache': 'prepared once per step per distinct key (inside the timed step)' if key_cache
+                   else 'off', 'tampered': int(tamper.sum()),
                    'parallelism': 'dp{} (disjoint index shards) + RCCL all-gather of verdict bitmaps'.format(world)
                    if world > 1 else 'single GPU'},
         'verdict_mismatches': mism,
@@ -336,8 +347,11 @@ def main():
                      'achieved': round(achieved / 1e12, 3), 'peak': round(peak / 1e12, 3),
                      'unit': 'Tmad/s (v_mad_u64_u32 lane-ops)', 'frac': round(achieved / peak, 4),
                      'traffic': _traffic_per_launch() if (args.config, n) == ('c2', CONFIGS['c2']['n']) else None,
-                     'work_per_verify': {'fe_mul': W_MUL_PER_VERIFY, 'fe_sq': W_SQ_PER_VERIFY,
-                                         'mad': W_MAD_PER_VERIFY}},
+                     'work_per_verify': ({'fe_mul': W_MUL_KEYED, 'fe_sq': W_SQ_KEYED, 'mad': W_MAD_KEYED,
+                                          'per_distinct_key': {'fe_mul': W_MUL_KEYPREP, 'fe_sq': W_SQ_KEYPREP}}
+                                         if key_cache else
+                                         {'fe_mul': W_MUL_PER_VERIFY, 'fe_sq': W_SQ_PER_VERIFY,
+                                          'mad': W_MAD_PER_VERIFY})},
         'cpu_baseline': None,
     }
     if tally is not None:

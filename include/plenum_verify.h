@@ -59,6 +59,15 @@ extern "C" {
 
 /* flags for pv_verify_batch */
 #define PV_FLAG_NONE 0u
+/* Deduplicate verifying keys on the host and prepare each distinct key once
+ * (decompressed -A and its cached multiples) when at least half of a shard's
+ * signatures repeat a key (node COMMIT votes, many requests per client DID).
+ * Verdicts are identical; only the work changes. */
+#define PV_FLAG_DEDUP_KEYS 1u
+
+/* words per prepared key (pv_keys_prepare_device): 9 cached multiples of -A
+ * (40 words each) + status word (+ padding) */
+#define PV_KEY_WORDS 368u
 
 /* Initialise the engine on the GPUs in device_mask (bit d = HIP device d;
  * 0 = all visible devices).  Idempotent.  Builds the base-point table. */
@@ -88,6 +97,21 @@ int pv_verify_batch(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_bl
  * word i/64 = verdict i (the layout all-gathered across ranks). */
 int pv_verify_batch_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
                            uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device, void *stream);
+
+/* Verifying-key cache on the device.  pv_keys_prepare_device fills ktab
+ * (k x PV_KEY_WORDS words) for the k 32-byte keys in pk; a key that libsodium
+ * would refuse (non-canonical, small order, not on the curve) is marked so and
+ * every signature under it is rejected.  pv_verify_keyed_device verifies n
+ * signatures whose key is pk[key_idx[i]] (the same pk array the table was built
+ * from: the hash still covers the key's bytes) — same verdicts as
+ * pv_verify_batch_device on the gathered keys, without re-decompressing a key
+ * per signature.  Replaces the per-call VerifyKey(key) construction of
+ * stp_core/crypto/nacl_wrappers.py:71-81 for repeated keys. */
+int pv_keys_prepare_device(const uint8_t *pk, uint64_t k, uint32_t *ktab, int device, void *stream);
+
+int pv_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk, const uint8_t *sig,
+                           const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n, uint8_t *verdict,
+                           uint64_t *bitmap, int device, void *stream);
 
 /* Per-batch quorum tally (HOST memory).
  *   verdict    n_msgs bytes (1 = vote counts)
@@ -146,6 +170,12 @@ int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, 
 int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
                           uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device, void *stream, int iters,
                           float *ms_hash, float *ms_curve);
+
+/* pv_time_verify_device for keyed batches. */
+int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk, const uint8_t *sig,
+                                const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n, uint8_t *verdict,
+                                uint64_t *bitmap, int device, void *stream, int iters, float *ms_hash,
+                                float *ms_curve);
 
 #ifdef __cplusplus
 }

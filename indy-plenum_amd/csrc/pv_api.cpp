@@ -12,10 +12,13 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/plenum_verify.h"
 #include "pv_kernels.h"
+
+static_assert(PV_KEY_WORDS == (unsigned)pv::KEYTAB_WORDS, "prepared-key layout");
 
 namespace {
 
@@ -77,6 +80,7 @@ struct Device {
   DevBuf<uint32_t> sender, votes;
   DevBuf<uint8_t> reached;
   DevBuf<uint64_t> scan;      // block sums of the device prefix scan
+  DevBuf<uint32_t> ktab, kidx;  // prepared keys + per-signature key index (deduplicated host batches)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -132,6 +136,7 @@ void release_device(Device& d) {
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.bitmap.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
+  d.ktab.release(); d.kidx.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -142,7 +147,7 @@ void release_device(Device& d) {
 // enqueue hash + curve for device-resident inputs on stream s
 int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
                    uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed, float* ms_hash,
-                   float* ms_curve) {
+                   float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
   if (n == 0) return PV_OK;
   HIP_OK(d.h.ensure(n * 16));
   HIP_OK(d.pre.ensure(n));
@@ -152,10 +157,10 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
     bm = d.bitmap.p;
   }
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
-  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.counter.p, d.h.p, d.pre.p, d.hash_blocks, s));
+  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.counter.p, d.h.p, d.pre.p, d.hash_blocks, s, kidx));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict, bm,
-                          n, d.curve_blocks, s));
+                          n, d.curve_blocks, s, ktab, kidx));
   if (timed) {
     HIP_OK(hipEventRecord(d.ev[2], s));
     HIP_OK(hipEventSynchronize(d.ev[2]));
@@ -218,7 +223,7 @@ int pv_device_count(void) {
 
 int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off,
                     uint64_t n, uint8_t* verdict, uint32_t device_mask, uint32_t flags) {
-  (void)flags;
+  if (flags & ~PV_FLAG_DEDUP_KEYS) return fail(PV_EINVAL, "unknown flags 0x%x", flags);
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceGuard dg;
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
@@ -240,19 +245,57 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     const uint64_t b0 = msg_off[s], bytes = msg_off[e] - b0;
     offs[g].resize(m + 1);
     for (uint64_t k = 0; k <= m; ++k) offs[g][k] = msg_off[s + k] - b0;
-    HIP_OK(d.pk.ensure(m * 32));
+    // PV_FLAG_DEDUP_KEYS: prepare each distinct key once (cached multiples of
+    // -A) when at least half of the shard's signatures repeat a key
+    uint64_t nk = m;
+    std::vector<uint8_t> upk;
+    std::vector<uint32_t> idx;
+    if (flags & PV_FLAG_DEDUP_KEYS) {
+      struct KeyHash {
+        size_t operator()(const std::string& k) const {
+          uint64_t h;
+          memcpy(&h, k.data(), 8);
+          return (size_t)h;
+        }
+      };
+      std::unordered_map<std::string, uint32_t, KeyHash> seen;
+      seen.reserve(m);
+      idx.resize(m);
+      for (uint64_t k = 0; k < m; ++k) {
+        auto it = seen.emplace(std::string(reinterpret_cast<const char*>(pk + 32 * (s + k)), 32), (uint32_t)seen.size());
+        if (it.second) upk.insert(upk.end(), pk + 32 * (s + k), pk + 32 * (s + k) + 32);
+        idx[k] = it.first->second;
+      }
+      nk = seen.size();
+      if (2 * nk > m) {
+        nk = m;
+        idx.clear();
+      }
+    }
+    const bool keyed = !idx.empty();
+    HIP_OK(d.pk.ensure((keyed ? nk : m) * 32));
     HIP_OK(d.sig.ensure(m * 64));
     HIP_OK(d.blob.ensure(bytes + 16));
     HIP_OK(d.off.ensure(m + 1));
     HIP_OK(d.verdict.ensure(m));
-    HIP_OK(hipMemcpyAsync(d.pk.p, pk + 32 * s, m * 32, hipMemcpyHostToDevice, d.stream));
+    if (keyed) {
+      HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
+      HIP_OK(d.kidx.ensure(m));
+      HIP_OK(hipMemcpyAsync(d.pk.p, upk.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
+      HIP_OK(hipMemcpyAsync(d.kidx.p, idx.data(), m * 4, hipMemcpyHostToDevice, d.stream));
+      HIP_OK(pv::launch_keys(d.pk.p, nk, d.ktab.p, d.stream));
+    } else {
+      HIP_OK(hipMemcpyAsync(d.pk.p, pk + 32 * s, m * 32, hipMemcpyHostToDevice, d.stream));
+    }
     HIP_OK(hipMemcpyAsync(d.sig.p, sig + 64 * s, m * 64, hipMemcpyHostToDevice, d.stream));
     if (bytes) HIP_OK(hipMemcpyAsync(d.blob.p, msg_blob + b0, bytes, hipMemcpyHostToDevice, d.stream));
     HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.stream));
     HIP_OK(hipMemcpyAsync(d.off.p, offs[g].data(), (m + 1) * 8, hipMemcpyHostToDevice, d.stream));
     int rc = enqueue_verify(d, d.pk.p, d.sig.p, d.blob.p, d.off.p, m, d.verdict.p, nullptr, d.stream, false, nullptr,
-                            nullptr);
+                            nullptr, keyed ? d.ktab.p : nullptr, keyed ? d.kidx.p : nullptr);
     if (rc) return rc;
+    // the key staging vectors die with this iteration: drain the shard's copies first
+    if (keyed) HIP_OK(hipStreamSynchronize(d.stream));
     HIP_OK(hipMemcpyAsync(verdict + s, d.verdict.p, m, hipMemcpyDeviceToHost, d.stream));
   }
   for (uint64_t g = 0; g < G; ++g) {
@@ -275,6 +318,58 @@ int pv_verify_batch_device(const uint8_t* pk, const uint8_t* sig, const uint8_t*
   int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr);
   if (rc) return rc;
   HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_keys_prepare_device(const uint8_t* pk, uint64_t k, uint32_t* ktab, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (k == 0) return PV_OK;
+  if (!pk || !ktab) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(pv::launch_keys(pk, k, ktab, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const uint8_t* pk, const uint8_t* sig,
+                           const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n, uint8_t* verdict,
+                           uint64_t* bitmap, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n == 0) return PV_OK;
+  if (!ktab || !key_idx || !pk || !sig || !msg_blob || !msg_off || !verdict) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr, ktab, key_idx);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_time_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const uint8_t* pk, const uint8_t* sig,
+                                const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n, uint8_t* verdict,
+                                uint64_t* bitmap, int device, void* stream, int iters, float* ms_hash,
+                                float* ms_curve) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (iters <= 0) return fail(PV_EINVAL, "iters must be > 0");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  float a = 0, b = 0;
+  for (int it = 0; it < iters; ++it) {
+    int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, true, &a, &b, ktab, key_idx);
+    if (rc) return rc;
+  }
+  if (ms_hash) *ms_hash = a / iters;
+  if (ms_curve) *ms_curve = b / iters;
   return PV_OK;
 }
 

@@ -31,14 +31,22 @@ hipError_t curve_occupancy(int* blocks_per_cu);
 // kernel).  Persistent grid of `blocks` blocks; `counter` is an 8-byte device
 // word the launch resets (work queue).
 hipError_t hash_occupancy(int* blocks_per_cu);
+// kidx (may be NULL): signature i's key is pk[kidx[i]] (keyed batches)
 hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
-                       unsigned long long* counter, uint32_t* dig, uint8_t* pre, int blocks, hipStream_t s);
+                       unsigned long long* counter, uint32_t* dig, uint8_t* pre, int blocks, hipStream_t s,
+                       const uint32_t* kidx = nullptr);
 
 // verdict[i] in {0,1}; bitmap[i/64] bit i%64 (bitmap must hold ceil(n/64) words);
 // h = the hash kernel's digests (16 words per signature)
+// ktab/kidx (may be NULL): keyed mode, signature i uses prepared key kidx[i]
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
-                        uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s);
+                        uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab = nullptr,
+                        const uint32_t* kidx = nullptr);
+
+// prepared keys: KEY_WORDS words per key (table of k*(-A) + status)
+constexpr int KEYTAB_WORDS = 9 * 40 + 8;
+hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, hipStream_t s);
 
 // keygen + sign: pk[i], sig[i] for seed[i] over M_i
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n,

@@ -24,7 +24,8 @@ namespace pv {
 #define PV_CURVE_WAVES 2
 #endif
 
-static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS, "table layout");
+static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
+                  KEY_WORDS == KEYTAB_WORDS, "table layout");
 
 // ------------------------------------------------------------- hash kernel
 // Persistent lanes with per-lane refill: each lane runs ONE SHA-512
@@ -51,14 +52,17 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
                                                      const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ off, uint64_t n,
                                                      unsigned long long* __restrict__ counter,
-                                                     uint32_t* __restrict__ dig, uint8_t* __restrict__ pre) {
+                                                     uint32_t* __restrict__ dig, uint8_t* __restrict__ pre,
+                                                     const uint32_t* __restrict__ kidx) {
   uint64_t idx = take_index(counter);
   uint64_t blk = 0, nblk = 0, mo = 0, ml = 0;
   uint64_t hs[8];
+  const uint8_t* A = pk;
   while (true) {
     // refill: skip messages that fail the pre-checks
     while (blk == nblk && idx < n) {
-      const bool ok = precheck(pk + 32 * idx, sig + 64 * idx);
+      A = pk + 32 * (kidx ? (uint64_t)kidx[idx] : idx);
+      const bool ok = precheck(A, sig + 64 * idx);
       pre[idx] = ok ? 1 : 0;
       if (ok) {
         mo = off[idx];
@@ -72,7 +76,7 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
     }
     if (idx >= n) break;
     uint64_t w[16];
-    hram_block(w, sig + 64 * idx, pk + 32 * idx, blob + mo, ml, blk, nblk);
+    hram_block(w, sig + 64 * idx, A, blob + mo, ml, blk, nblk);
     sha512_compress(hs, w);
     if (++blk == nblk) {
       uint32_t d[16];
@@ -91,13 +95,15 @@ hipError_t hash_occupancy(int* blocks_per_cu) {
 }
 
 hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
-                       unsigned long long* counter, uint32_t* dig, uint8_t* pre, int blocks, hipStream_t s) {
+                       unsigned long long* counter, uint32_t* dig, uint8_t* pre, int blocks, hipStream_t s,
+                       const uint32_t* kidx) {
   if (n == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
   const uint64_t need = (n + HASH_BLOCK - 1) / HASH_BLOCK;
   const uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
-  hipLaunchKernelGGL(k_hash, dim3((uint32_t)b), dim3(HASH_BLOCK), 0, s, pk, sig, blob, off, n, counter, dig, pre);
+  hipLaunchKernelGGL(k_hash, dim3((uint32_t)b), dim3(HASH_BLOCK), 0, s, pk, sig, blob, off, n, counter, dig, pre,
+                     kidx);
   return hipGetLastError();
 }
 
@@ -117,6 +123,7 @@ hipError_t launch_btable_init(uint32_t* btab, hipStream_t s) {
 // points awaiting the shared inversion) and takes CURVE_K signatures per round:
 // gid, gid + nthreads, ... , gid + (K-1) nthreads.  Each wavefront covers 64
 // consecutive signatures per k, so each ballot is one aligned bitmap word.
+template <bool KEYED>
 __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uint8_t* __restrict__ pk,
                                                                         const uint8_t* __restrict__ sig,
                                                                         const uint32_t* __restrict__ hin,
@@ -124,7 +131,9 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
                                                                         const uint32_t* __restrict__ btab_g,
                                                                         uint32_t* __restrict__ scratch,
                                                                         uint8_t* __restrict__ verdict,
-                                                                        uint64_t* __restrict__ bitmap, uint64_t n) {
+                                                                        uint64_t* __restrict__ bitmap, uint64_t n,
+                                                                        const uint32_t* __restrict__ ktab,
+                                                                        const uint32_t* __restrict__ kidx) {
   __shared__ uint32_t btab[BTAB_ENTRIES * BTAB_WORDS];
   for (int j = threadIdx.x; j < BTAB_ENTRIES * BTAB_WORDS; j += CURVE_BLOCK) btab[j] = btab_g[j];
   __syncthreads();
@@ -132,7 +141,8 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
   const uint64_t gid = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
   uint32_t* lane = scratch + gid * LANE_WORDS;
   for (uint64_t base = 0; base < n; base += CURVE_K * nthreads) {
-    const uint32_t okm = curve_group(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab);
+    const uint32_t okm = KEYED ? curve_group(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx)
+                               : curve_group(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab);
 #pragma unroll
     for (int k = 0; k < CURVE_K; ++k) {
       const uint64_t i = base + (uint64_t)k * nthreads + gid;
@@ -147,20 +157,37 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
 }
 
 hipError_t curve_occupancy(int* blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_curve),
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_curve<false>),
                                                       CURVE_BLOCK, 0);
 }
 
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
-                        uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s) {
+                        uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab,
+                        const uint32_t* kidx) {
   if (n == 0) return hipSuccess;
   uint64_t need = (n + (uint64_t)CURVE_BLOCK * CURVE_K - 1) / ((uint64_t)CURVE_BLOCK * CURVE_K);
   uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
   if (b * CURVE_BLOCK > scratch_lanes) b = scratch_lanes / CURVE_BLOCK;
   if (b == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_curve, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch, verdict,
-                     bitmap, n);
+  if (ktab)
+    hipLaunchKernelGGL(k_curve<true>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
+                       verdict, bitmap, n, ktab, kidx);
+  else
+    hipLaunchKernelGGL(k_curve<false>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
+                       verdict, bitmap, n, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+// -------------------------------------------------------------- key cache
+__global__ __launch_bounds__(256) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < k) key_prepare(ktab + j * KEY_WORDS, pk + 32 * j);
+}
+
+hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_keys, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, s, pk, k, ktab);
   return hipGetLastError();
 }
 

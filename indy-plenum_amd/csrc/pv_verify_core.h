@@ -397,6 +397,46 @@ PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const u
   return true;
 }
 
+// ------------------------------------------------------------- key cache
+// One verifying key, prepared once and shared by every signature under it:
+// the 9-entry table of cached multiples k*(-A) (AT_WORDS) and a status word
+// (1 = A canonical, not small order, decompresses; SURVEY.md App. C.2 steps
+// 2-4).  KEY_WORDS per key in HBM.
+constexpr int KEY_STATUS = AT_WORDS;
+constexpr int KEY_WORDS = AT_WORDS + 8;
+
+PV_HD void key_prepare(uint32_t* kt, const uint8_t* pk) {
+  uint32_t A[8];
+  load8(A, pk);
+  ge_p3 negA;
+  bool ok = y_is_canonical(A) && !has_small_order(A) && ge_frombytes_negate(negA, A);
+  if (ok) {
+    build_atab(kt, negA);
+  } else {
+#pragma unroll 1
+    for (int k = 0; k < AT_WORDS; ++k) kt[k] = 0;
+  }
+#pragma unroll
+  for (int k = AT_WORDS; k < KEY_WORDS; ++k) kt[k] = 0;
+  kt[KEY_STATUS] = ok ? 1u : 0u;
+}
+
+// R' = h(-A) + S B with -A's table taken from a prepared key
+PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, const uint32_t* dig_src,
+                             const uint32_t* btab) {
+  if (!kt[KEY_STATUS]) return false;
+  uint32_t hh[8], S[8];
+  {
+    uint32_t dig[16];
+    load8(dig, reinterpret_cast<const uint8_t*>(dig_src));
+    load8(dig + 8, reinterpret_cast<const uint8_t*>(dig_src + 8));
+    sc_reduce64(hh, dig);
+  }
+  load8(S, sig + 32);
+  double_scalarmult(rp, hh, S, kt, btab);
+  return true;
+}
+
 // Signatures one lane finishes together: their final Z^-1 share ONE field
 // inversion (Montgomery's trick: 3(K-1) multiplies + 1 inversion instead of
 // K inversions).
@@ -430,8 +470,10 @@ PV_HD void batch_invert_z(uint32_t* pts, int K) {
 // One lane's group of CURVE_K signatures i0, i0 + stride, ...: returns the
 // accepted bitmask.  Rejected or absent entries carry Z = 1 through the
 // shared inversion.  scratch = LANE_WORDS words owned by this lane.
+// Keyed mode (ktab != nullptr): signature i uses prepared key kidx[i].
 PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre, uint64_t i0,
-                           uint64_t stride, uint64_t n, uint32_t* scratch, const uint32_t* btab) {
+                           uint64_t stride, uint64_t n, uint32_t* scratch, const uint32_t* btab,
+                           const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
   uint32_t* pts = scratch + AT_WORDS;
   uint32_t live = 0;
 #pragma unroll 1
@@ -439,7 +481,12 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     const uint64_t i = i0 + (uint64_t)k * stride;
     ge_p2 rp;
     bool ok = false;
-    if (i < n && pre[i]) ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);
+    if (i < n && pre[i]) {
+      if (ktab)
+        ok = curve_point_keyed(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, btab);
+      else
+        ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);
+    }
     if (!ok) {
       fe_0(rp.X);
       fe_0(rp.Y);

@@ -41,6 +41,12 @@ SIGNATURES = [
     ('pv_synth_fill_device', ctypes.c_int,
      [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp,
       _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_keys_prepare_device', ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp]),
+    ('pv_verify_keyed_device', ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_time_verify_keyed_device', ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int,
+      ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ('pv_time_verify_device', ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int,
       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
@@ -128,8 +134,15 @@ def pack_messages(msgs):
     return blob, off
 
 
-def verify_batch_arrays(pk, sig, blob, off, device_mask=0):
-    """pk (n,32) u8, sig (n,64) u8, blob u8, off (n+1) u64 -> verdict (n,) bool."""
+PV_FLAG_DEDUP_KEYS = 1
+PV_KEY_WORDS = 368
+
+
+def verify_batch_arrays(pk, sig, blob, off, device_mask=0, dedup_keys=True):
+    """pk (n,32) u8, sig (n,64) u8, blob u8, off (n+1) u64 -> verdict (n,) bool.
+
+    dedup_keys: let the library prepare each distinct key once when keys repeat
+    (PV_FLAG_DEDUP_KEYS; same verdicts)."""
     ensure_init()
     pk = np.ascontiguousarray(pk, dtype=np.uint8)
     sig = np.ascontiguousarray(sig, dtype=np.uint8)
@@ -143,8 +156,9 @@ def verify_batch_arrays(pk, sig, blob, off, device_mask=0):
     verdict = np.zeros(n, dtype=np.uint8)
     if n == 0:
         return verdict.astype(bool)
+    flags = PV_FLAG_DEDUP_KEYS if dedup_keys else 0
     _check('pv_verify_batch', load().pv_verify_batch(_ptr(pk), _ptr(sig), _ptr(blob), _ptr(off), n, _ptr(verdict),
-                                                      device_mask, 0))
+                                                      device_mask, flags))
     return verdict.astype(bool)
 
 

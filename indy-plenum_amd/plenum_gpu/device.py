@@ -31,7 +31,7 @@ class SyntheticBatch:
         nat.ensure_init(1 << self.device.index)
         dev = self.device
         self.n, self.mlen, self.cfg, self.first, self.mode = n, mlen, cfg, first, mode
-        self.n_nodes = n_nodes
+        self.n_nodes, self.key_mod = n_nodes, key_mod
         mlen_max = mlen if mlen_max is None else mlen_max
         u8 = dict(dtype=torch.uint8, device=dev)
         lib = nat.load()
@@ -52,10 +52,64 @@ class SyntheticBatch:
                    lib.pv_synth_fill_device(cfg, mode, first, n, key_mod, n_nodes, _p(self.off), _p(self.blob),
                                             _p(self.seeds), _p(self.pk), _p(self.sig), _p(self.tamper),
                                             _p(self.sender), dev.index, _stream(dev)))
+        self.keys = None   # (unique pk (k,32), key index (n,)) once use_key_cache() ran
+        self.ktab = None
+
+    def key_index(self):
+        """(unique keys, key index) of this batch from the synth spec: COMMIT
+        votes use the sender node's key, a key pool key (first + j) mod key_mod."""
+        dev = self.device
+        if self.mode == 2:
+            k = self.n_nodes
+            kidx = self.sender.to(torch.int64)
+        elif self.key_mod:
+            k = min(self.key_mod, self.n)
+            kidx = (torch.arange(self.n, dtype=torch.int64, device=dev) + self.first) % self.key_mod
+        else:
+            return None
+        # one signature per key holds its bytes: the first occurrence
+        first = torch.full((k if self.mode == 2 else self.key_mod,), -1, dtype=torch.int64, device=dev)
+        pos = torch.arange(self.n, dtype=torch.int64, device=dev)
+        first.scatter_reduce_(0, kidx, pos, reduce='amin', include_self=False)
+        if (first < 0).any():
+            # key pool larger than the batch: index only the keys present
+            present = torch.nonzero(first >= 0).flatten()
+            remap = torch.full_like(first, -1)
+            remap[present] = torch.arange(present.numel(), device=dev)
+            kidx = remap[kidx]
+            first = first[present]
+        return self.pk[first].contiguous(), kidx.to(torch.int32).contiguous()
+
+    def use_key_cache(self, on=True):
+        """Verify through prepared keys (pv_keys_prepare_device + keyed kernels)."""
+        if not on:
+            self.keys = self.ktab = None
+            return False
+        ki = self.key_index()
+        if ki is None:
+            return False
+        self.keys = ki
+        self.ktab = torch.empty(ki[0].shape[0] * nat.PV_KEY_WORDS, dtype=torch.int32, device=self.device)
+        return True
+
+    def prepare_keys(self):
+        upk, _ = self.keys
+        nat._check('pv_keys_prepare_device',
+                   nat.load().pv_keys_prepare_device(_p(upk), upk.shape[0], _p(self.ktab), self.device.index,
+                                                     _stream(self.device)))
 
     def verify(self):
-        """One pass of the hot path over the batch (hash + curve kernels)."""
+        """One pass of the hot path over the batch (hash + curve kernels; with
+        the key cache: key preparation + keyed hash + keyed curve)."""
         lib = nat.load()
+        if self.keys is not None:
+            self.prepare_keys()
+            upk, kidx = self.keys
+            nat._check('pv_verify_keyed_device',
+                       lib.pv_verify_keyed_device(_p(self.ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob),
+                                                  _p(self.off), self.n, _p(self.verdict), _p(self.bitmap),
+                                                  self.device.index, _stream(self.device)))
+            return self.verdict
         nat._check('pv_verify_batch_device',
                    lib.pv_verify_batch_device(_p(self.pk), _p(self.sig), _p(self.blob), _p(self.off), self.n,
                                               _p(self.verdict), _p(self.bitmap), self.device.index,
@@ -66,6 +120,14 @@ class SyntheticBatch:
         """Average (hash_ms, curve_ms) per launch from HIP events on the launch stream."""
         lib = nat.load()
         a, b = ctypes.c_float(), ctypes.c_float()
+        if self.keys is not None:
+            upk, kidx = self.keys
+            nat._check('pv_time_verify_keyed_device',
+                       lib.pv_time_verify_keyed_device(_p(self.ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob),
+                                                       _p(self.off), self.n, _p(self.verdict), _p(self.bitmap),
+                                                       self.device.index, _stream(self.device), iters,
+                                                       ctypes.byref(a), ctypes.byref(b)))
+            return a.value, b.value
         nat._check('pv_time_verify_device',
                    lib.pv_time_verify_device(_p(self.pk), _p(self.sig), _p(self.blob), _p(self.off), self.n,
                                              _p(self.verdict), _p(self.bitmap), self.device.index,

@@ -117,3 +117,46 @@ def test_sign_matches_oracle_and_fixture(nat, raw_vectors):
     blob, off = nat.pack_messages(msgs)
     pk, sig = nat.sign_batch_arrays(seeds, blob, off)
     assert (pk == r['pk'][idx]).all() and (sig == r['sig'][idx]).all()
+
+
+def _adv_soa(adversarial, reps=1):
+    rows = [(pk, sm, v) for _, pk, sm, v in split_sm(adversarial) if len(sm) >= 64] * reps
+    pk = np.frombuffer(b''.join(r[0] for r in rows), np.uint8).reshape(-1, 32)
+    sig = np.frombuffer(b''.join(r[1][:64] for r in rows), np.uint8).reshape(-1, 64)
+    blob, off = orc_pack([r[1][64:] for r in rows])
+    return pk, sig, blob, off, np.array([r[2] for r in rows])
+
+
+def orc_pack(msgs):
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    return np.frombuffer(b''.join(msgs), np.uint8), off
+
+
+@pytest.mark.parametrize('dedup', [False, True])
+def test_adversarial_prepared_keys(nat, adversarial, dedup):
+    """Every adversarial row three times: with PV_FLAG_DEDUP_KEYS each
+    distinct key (small order, non-canonical, off-curve, mixed order ...) is
+    prepared once on the device; verdicts equal the fixture either way."""
+    pk, sig, blob, off, want = _adv_soa(adversarial, reps=3)
+    got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=dedup)
+    assert (got == want).all()
+
+
+def test_keyed_device_path_c3_and_c4(nat):
+    """Device key cache (pv_keys_prepare_device + pv_verify_keyed_device) on
+    COMMIT votes (25 node keys) and on a 4096-key pool with ragged payloads:
+    identical verdicts to the unkeyed path, == not tampered."""
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch
+    for b in (SyntheticBatch(0, 25 * 4000, 0, cfg=3, first=25 * 77, mode=synth.COMMIT, n_nodes=25),
+              SyntheticBatch(0, 60000, 128, cfg=4, first=12345, key_mod=4096, mode=synth.RANGE, mlen_max=4096)):
+        v0 = b.verify().cpu().numpy().copy()
+        assert b.use_key_cache()
+        v1 = b.verify().cpu().numpy()
+        assert (v0 == v1).all()
+        assert (v1.astype(bool) == ~b.tamper.cpu().numpy().astype(bool)).all()
+        bits = np.unpackbits(b.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:b.n]
+        assert (bits == v1).all()
+        th, tc = b.time_kernels(1)
+        assert th > 0 and tc > 0

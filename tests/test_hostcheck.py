@@ -180,3 +180,66 @@ print('ok', len(rows))
     r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert 'runtime error' not in r.stderr, r.stderr
+
+
+def _adv_arrays(adversarial):
+    """adversarial fixture as SoA arrays with the reference's sig||msg framing (len(sm) >= 64 only)."""
+    rows = [(pk, sm, v) for _, pk, sm, v in split_sm(adversarial) if len(sm) >= 64]
+    pk = np.frombuffer(b''.join(r[0] for r in rows), np.uint8).reshape(-1, 32)
+    sig = np.frombuffer(b''.join(r[1][:64] for r in rows), np.uint8).reshape(-1, 64)
+    msgs = [r[1][64:] for r in rows]
+    off = np.zeros(len(rows) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    return pk, sig, np.frombuffer(b''.join(msgs), np.uint8), off, np.array([r[2] for r in rows])
+
+
+def test_keyed_path_adversarial_bit_exact(hc, adversarial):
+    """Prepared-key path (key_prepare + keyed curve): every adversarial key
+    (small order, non-canonical, off-curve, mixed order) and signature gives
+    the fixture's verdict."""
+    pk, sig, blob, off, want = _adv_arrays(adversarial)
+    upk, kidx = np.unique(pk, axis=0, return_inverse=True)
+    kidx = np.ascontiguousarray(kidx.reshape(-1), np.uint32)
+    upk = np.ascontiguousarray(upk, np.uint8)
+    n = len(pk)
+    v = np.zeros(n, np.uint8)
+    b = orc.padded(blob)
+    hc.hc_reset_counts()
+    sig = np.ascontiguousarray(sig)
+    off = np.ascontiguousarray(off)
+    hc.hc_verify_keyed(_p(upk), ctypes.c_uint64(len(upk)), _p(kidx), _p(sig), _p(b), _p(off), ctypes.c_uint64(n), _p(v))
+    _, bad = counts(hc)
+    assert bad == 0
+    assert (v.astype(bool) == want).all()
+
+
+def test_op_counts_pin_keyed_constants(hc):
+    """Work split of the prepared-key path (bench.py W_*_KEYED / W_*_KEYPREP):
+    16 signatures under ONE prepared key vs 16 keys prepared."""
+    import bench
+    n = 16
+    seeds = np.frombuffer(os.urandom(32 * n), np.uint8).reshape(n, 32)
+    blob = np.frombuffer(os.urandom(256 * n), np.uint8)
+    off = np.arange(n + 1, dtype=np.uint64) * 256
+    pk, sig = orc.sign_batch(seeds, blob, off)
+    hc.hc_btable((ctypes.c_uint32 * (129 * 32))())
+    v = np.zeros(n, np.uint8)
+
+    def run(upk, kidx, s, b):
+        bp = orc.padded(b)   # keep the buffer alive across the call
+        hc.hc_reset_counts()
+        hc.hc_verify_keyed(_p(upk), ctypes.c_uint64(len(upk)), _p(kidx), _p(s), _p(bp), _p(off),
+                           ctypes.c_uint64(n), _p(v))
+        assert v.all()
+        c, bad = counts(hc)
+        assert bad == 0
+        return c
+    c_many = run(np.ascontiguousarray(pk), np.arange(n, dtype=np.uint32), np.ascontiguousarray(sig), blob)
+    one = np.ascontiguousarray(pk[:1])
+    c_one = run(one, np.zeros(n, np.uint32), np.ascontiguousarray(np.repeat(sig[:1], n, 0)), np.tile(blob[:256], n))
+    prep_sq = (int(c_many[1]) - int(c_one[1])) / (n - 1)
+    assert prep_sq == bench.W_SQ_KEYPREP
+    assert (int(c_one[1]) - prep_sq) / n == bench.W_SQ_KEYED
+    prep_mul = (int(c_many[0]) - int(c_one[0])) / (n - 1)
+    assert abs(prep_mul - bench.W_MUL_KEYPREP) <= 0.5
+    assert abs((int(c_one[0]) - prep_mul) / n - bench.W_MUL_KEYED) <= 0.1

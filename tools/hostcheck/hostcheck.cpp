@@ -85,6 +85,26 @@ void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
   free(pre);
 }
 
+// keyed variant: prepare each key of pk (k keys) once, signature i uses key kidx[i]
+void hc_verify_keyed(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig, const uint8_t* blob,
+                     const uint64_t* off, uint64_t n, uint8_t* verdict) {
+  ensure_btab();
+  static uint32_t lane[LANE_WORDS];
+  uint32_t* ktab = (uint32_t*)calloc(k ? k * KEY_WORDS : KEY_WORDS, sizeof(uint32_t));
+  for (uint64_t j = 0; j < k; ++j) key_prepare(ktab + j * KEY_WORDS, pk + 32 * j);
+  uint32_t* h = (uint32_t*)calloc(n ? n * 16 : 16, sizeof(uint32_t));
+  uint8_t* pre = (uint8_t*)calloc(n ? n : 1, 1);
+  for (uint64_t i = 0; i < n; ++i)
+    pre[i] = hash_one(h + 16 * i, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+  for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
+    const uint32_t okm = curve_group(pk, sig, h, pre, i0, 1, n, lane, g_btab, ktab, kidx);
+    for (int q = 0; q < CURVE_K && i0 + q < n; ++q) verdict[i0 + q] = (okm >> q) & 1u;
+  }
+  free(ktab);
+  free(h);
+  free(pre);
+}
+
 void hc_sign_batch(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* pk,
                    uint8_t* sig) {
   ensure_btab();
