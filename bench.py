@@ -272,7 +272,8 @@ def main():
         q = Quorums(n_nodes).commit.value
         tally = dict(nb=nb, q=q, boff=torch.arange(nb + 1, dtype=torch.int64, device=dev) * n_nodes,
                      votes=torch.empty(nb, dtype=torch.int32, device=dev),
-                     reached=torch.empty(nb, dtype=torch.uint8, device=dev))
+                     reached=torch.empty(nb, dtype=torch.uint8, device=dev),
+                     gathered=torch.empty(world * nb, dtype=torch.uint8, device=dev))
 
     def step():
         batch.verify()
@@ -281,6 +282,8 @@ def main():
                          tally['reached'])
         if world > 1:
             dist.all_gather_into_tensor(gathered, batch.bitmap)
+            if tally is not None:   # C3: batch-sharded tallies, gather the quorum bits
+                dist.all_gather_into_tensor(tally['gathered'], tally['reached'])
 
     for _ in range(args.warmup):
         step()
@@ -311,6 +314,9 @@ def main():
         want_votes, want_reached = synth.c3_expected(rank * tally['nb'], tally['nb'], n_nodes, tally['q'])
         mism += int((tally['votes'].cpu().numpy() != want_votes.astype(np.int32)).sum())
         mism += int((tally['reached'].cpu().numpy().astype(bool) != want_reached).sum())
+        if world > 1:
+            _, all_reached = synth.c3_expected(0, world * tally['nb'], n_nodes, tally['q'])
+            mism += int((tally['gathered'].cpu().numpy().astype(bool) != all_reached).sum())
     if world > 1:
         allbits = np.unpackbits(gathered.cpu().numpy().view(np.uint8), bitorder='little')
         per = batch.bitmap.numel() * 64

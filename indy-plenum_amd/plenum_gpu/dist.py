@@ -66,3 +66,15 @@ def verify_sharded(pk, sig, blob, off, rank, world, verify_fn, group=None, devic
     if device is not None:
         bm = bm.to(device)
     return gather_verdicts(bm, n, world, group)
+
+
+def gather_quorums(reached_tensor, group=None):
+    """all_gather_into_tensor of each rank's per-batch quorum flags (uint8, one
+    per 3PC batch; every rank holds the same number of batches) -> bool[world*nb]
+    in global batch order (C3: batches shard by batch, the tally is rank-local)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    out = torch.empty(world * reached_tensor.numel(), dtype=reached_tensor.dtype, device=reached_tensor.device)
+    dist.all_gather_into_tensor(out, reached_tensor.contiguous(), group=group)
+    return out

@@ -70,3 +70,47 @@ def test_gloo_sharded_verify_allgather(world):
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(r, True) for r in range(world)], res
+
+
+def _tally_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, HERE)
+        import conftest  # noqa: F401
+        import torch
+        import torch.distributed as dist
+        from plenum_gpu import synth
+        from plenum_gpu.dist import gather_quorums
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        n_nodes, nb = 25, 300
+        # rank r owns 3PC batches [r*nb, (r+1)*nb): verdicts from the C3 spec, tally rank-local
+        # (the GPU tally kernel is covered by tests/test_gpu_tally.py; here the
+        # rank-local voter sets are counted in Python, the collective is real)
+        first = rank * nb
+        reached = np.zeros(nb, bool)
+        for j, b in enumerate(range(first, first + nb)):
+            snd, bad = synth.c3_slots(b, n_nodes)
+            reached[j] = len(set(snd[~bad].tolist())) >= 17
+        got = gather_quorums(torch.from_numpy(reached.astype(np.uint8))).numpy().astype(bool)
+        _, want = synth.c3_expected(0, world * nb, n_nodes, 17)
+        dist.destroy_process_group()
+        q.put((rank, bool((got == want).all())))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+
+
+def test_gloo_c3_quorum_bits_allgather():
+    """C3 over 2 ranks: batches shard by batch, each rank tallies its own, the
+    per-batch quorum bits are all-gathered and equal the spec's voter-set count."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tally_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert sorted(res) == [(r, True) for r in range(world)], res
