@@ -26,6 +26,13 @@ Fixtures
                         libsodium crypto_sign_open (framing included)
   tally.npz             25-node COMMIT batches: sender, verdict -> quorum bits via
                         the reference Commits/Quorums (plenum/server/models.py:91-114)
+  ingress.json          one node service pass for the batched-ingestion path (f1):
+                        client requests of every shape with the reference
+                        Request(**req).key (plenum/common/request.py:82-120) and the
+                        ReqAuthenticator outcome, PROPAGATE and BATCH wire dicts
+                        (Propagate/Batch._asdict, plenum/common/messages/node_messages.py)
+
+    PYTHONDONTWRITEBYTECODE=1 python oracle/gen_golden.py [fixture ...]   (default: all)
 """
 import ctypes
 import hashlib
@@ -635,18 +642,87 @@ def gen_tally(n_batches=500, n_nodes=25):
                 prepare_reached=np.array(prepare_reached, np.uint8))
 
 
-def main():
+def gen_ingress(n=48):
+    """One service pass: client requests (single/multi signature, optional
+    protocolVersion/taaAcceptance/endorser, tampered, unknown identifier), the
+    reference Request.key of each, the reference ReqAuthenticator outcome, and
+    PROPAGATE / BATCH wire dicts carrying some of them."""
+    from plenum.common.messages.node_messages import Batch, Propagate
+    from plenum.common.request import Request
+    rnd = random.Random(4242)
+    signers = [DidSigner(seed=det_seed(b'plenum-gpu/ingress', i)) for i in range(n + 8)]
+    authnr = CoreAuthNr(['buy'], [], [])
+    registry = {}
+    for s in signers[:n]:
+        authnr.addIdr(s.identifier, s.verkey)
+        registry[s.identifier] = s.verkey
+    ra = ReqAuthenticator()
+    ra.register_authenticator(authnr)
+    cases = []
+    for i in range(n):
+        s = signers[i]
+        req = {'identifier': s.identifier, 'reqId': 5000 + i,
+               'operation': {'type': 'buy', 'data': payload_chars(9000 + i, 40 + i)}, 'protocolVersion': 2}
+        kind = ['single', 'single', 'taa', 'endorser', 'multi', 'tampered', 'unknown', 'single'][i % 8]
+        if kind == 'taa':
+            req['taaAcceptance'] = {'mechanism': 'x', 'taaDigest': hashlib.sha256(b'taa%d' % i).hexdigest(),
+                                    'time': 1600000000 + 86400 * i}
+        if kind == 'endorser':
+            req['endorser'] = signers[(i + 1) % n].identifier
+        if kind == 'unknown':
+            s = signers[n + (i % 8)]
+            req['identifier'] = s.identifier
+        if kind in ('multi', 'endorser'):
+            other = signers[(i + 1) % n] if kind == 'endorser' else signers[(i + 3) % n]
+            sigs = {}
+            for sg in (s, other):
+                sigs[sg.identifier] = sg.sign(req)
+            req['signatures'] = sigs
+        else:
+            req['signature'] = s.sign(req)
+        if kind == 'tampered':
+            req['reqId'] += 1
+        key = Request(**req).key
+        try:
+            out = {'result': sorted(ra.authenticate(json.loads(json.dumps(req)), key=key))}
+        except Exception as ex:
+            out = exc_record(ex)
+        cases.append({'kind': kind, 'req': req, 'key': key, 'reqauth': out})
+    props = []
+    for i in range(0, n, 3):
+        props.append(json.loads(json.dumps(Propagate(cases[i]['req'], 'Client%d' % i)._asdict())))
+    batches = []
+    for j in range(0, len(props) - 2, 4):
+        msgs = [json.dumps(props[j + k]) for k in range(3)]
+        batches.append(json.loads(json.dumps(Batch(msgs, None)._asdict())))
+    rnd.shuffle(props)
+    return {'registry': registry, 'write_types': ['buy'], 'cases': cases, 'propagates': props, 'batches': batches}
+
+
+GENERATORS = ['kat', 'plenum_requests', 'raw_vectors', 'adversarial', 'tally', 'ingress']
+
+
+def main(which=None):
+    which = which or GENERATORS
     os.makedirs(OUT, exist_ok=True)
-    with open(os.path.join(OUT, 'kat.json'), 'w') as fh:
-        json.dump(gen_kat(), fh, indent=1, sort_keys=True)
-    with open(os.path.join(OUT, 'plenum_requests.json'), 'w') as fh:
-        json.dump(gen_plenum_requests(), fh, indent=0)  # keep dict order: the signature loop order matters
-    np.savez_compressed(os.path.join(OUT, 'raw_vectors.npz'), **gen_raw())
-    np.savez_compressed(os.path.join(OUT, 'adversarial.npz'), **gen_adversarial())
-    np.savez_compressed(os.path.join(OUT, 'tally.npz'), **gen_tally())
+    if 'kat' in which:
+        with open(os.path.join(OUT, 'kat.json'), 'w') as fh:
+            json.dump(gen_kat(), fh, indent=1, sort_keys=True)
+    if 'plenum_requests' in which:
+        with open(os.path.join(OUT, 'plenum_requests.json'), 'w') as fh:
+            json.dump(gen_plenum_requests(), fh, indent=0)  # keep dict order: the signature loop order matters
+    if 'raw_vectors' in which:
+        np.savez_compressed(os.path.join(OUT, 'raw_vectors.npz'), **gen_raw())
+    if 'adversarial' in which:
+        np.savez_compressed(os.path.join(OUT, 'adversarial.npz'), **gen_adversarial())
+    if 'tally' in which:
+        np.savez_compressed(os.path.join(OUT, 'tally.npz'), **gen_tally())
+    if 'ingress' in which:
+        with open(os.path.join(OUT, 'ingress.json'), 'w') as fh:
+            json.dump(gen_ingress(), fh, indent=0)
     for fn in sorted(os.listdir(OUT)):
         print(fn, os.path.getsize(os.path.join(OUT, fn)))
 
 
 if __name__ == '__main__':
-    main()
+    main(sys.argv[1:] or None)
