@@ -62,10 +62,11 @@ CONFIGS = {
 W_MUL_PER_VERIFY = 1581.5
 W_SQ_PER_VERIFY = 1326.5
 W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
-# keyed batches (prepared keys): the curve kernel skips decompression and the
-# table build; those run once per distinct key in the key-preparation kernel
-W_MUL_KEYED, W_SQ_KEYED = 1498.0, 1071.5
-W_MUL_KEYPREP, W_SQ_KEYPREP = 83.5, 255.0
+# keyed batches (prepared keys, 4-way comb of -A): 60 doublings instead of 256,
+# no decompression; decompression, the comb tables (3 x 61 doublings, 32 affine
+# multiples, one shared inversion) run once per distinct key in k_keys
+W_MUL_KEYED, W_SQ_KEYED = 858.0, 303.5
+W_MUL_KEYPREP, W_SQ_KEYPREP = 1031.0, 1241.0
 W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
 # v_mad_u64_u32 issue ceiling of one MI355X measured by tools/ubench/mad_peak.hip
 # (profiles/r01_mad_peak.json, best over 1..8 waves/SIMD): lane-ops/s, whole chip.

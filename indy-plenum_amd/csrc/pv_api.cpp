@@ -81,6 +81,8 @@ struct Device {
   DevBuf<uint8_t> reached;
   DevBuf<uint64_t> scan;      // block sums of the device prefix scan
   DevBuf<uint32_t> ktab, kidx;  // prepared keys + per-signature key index (deduplicated host batches)
+  DevBuf<uint32_t> kscr;        // key-preparation scratch
+  int curve_blocks_keyed = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -108,7 +110,7 @@ int init_device(Device& d) {
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d.id));
   d.cu_count = prop.multiProcessorCount;
-  HIP_OK(d.btab.ensure(pv::BTAB_ENTRIES * pv::BTAB_WORDS));
+  HIP_OK(d.btab.ensure(pv::BTAB_QUARTERS * pv::BTAB_ENTRIES * pv::BTAB_WORDS));
   HIP_OK(pv::launch_btable_init(d.btab.p, d.stream));
   // persistent curve grid: resident blocks per CU from the occupancy query
   // (kept <= 4 blocks of 256 threads per CU, see cdna_hip_programming.md §1)
@@ -118,6 +120,11 @@ int init_device(Device& d) {
   if (per_cu > 4) per_cu = 4;
   d.curve_blocks = d.cu_count * per_cu;
   HIP_OK(d.scratch.ensure((size_t)d.curve_blocks * pv::CURVE_BLOCK * pv::ATAB_WORDS));
+  int kper = 0;
+  HIP_OK(pv::curve_occupancy(&kper, true));
+  if (kper < 1) kper = 1;
+  if (kper > per_cu) kper = per_cu;
+  d.curve_blocks_keyed = d.cu_count * kper;
   int hper = 0;
   HIP_OK(pv::hash_occupancy(&hper));
   if (hper < 1) hper = 1;
@@ -136,7 +143,7 @@ void release_device(Device& d) {
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.bitmap.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
-  d.ktab.release(); d.kidx.release();
+  d.ktab.release(); d.kidx.release(); d.kscr.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -160,7 +167,7 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
   HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.counter.p, d.h.p, d.pre.p, d.hash_blocks, s, kidx));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict, bm,
-                          n, d.curve_blocks, s, ktab, kidx));
+                          n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx));
   if (timed) {
     HIP_OK(hipEventRecord(d.ev[2], s));
     HIP_OK(hipEventSynchronize(d.ev[2]));
@@ -283,7 +290,8 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
       HIP_OK(d.kidx.ensure(m));
       HIP_OK(hipMemcpyAsync(d.pk.p, upk.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
       HIP_OK(hipMemcpyAsync(d.kidx.p, idx.data(), m * 4, hipMemcpyHostToDevice, d.stream));
-      HIP_OK(pv::launch_keys(d.pk.p, nk, d.ktab.p, d.stream));
+      HIP_OK(d.kscr.ensure(nk * pv::KEYTAB_SCRATCH));
+      HIP_OK(pv::launch_keys(d.pk.p, nk, d.ktab.p, d.kscr.p, d.stream));
     } else {
       HIP_OK(hipMemcpyAsync(d.pk.p, pk + 32 * s, m * 32, hipMemcpyHostToDevice, d.stream));
     }
@@ -330,7 +338,8 @@ int pv_keys_prepare_device(const uint8_t* pk, uint64_t k, uint32_t* ktab, int de
   if (!pk || !ktab) return fail(PV_EINVAL, "null device buffer");
   HIP_OK(hipSetDevice(device));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
-  HIP_OK(pv::launch_keys(pk, k, ktab, s));
+  HIP_OK(d->kscr.ensure(k * pv::KEYTAB_SCRATCH));
+  HIP_OK(pv::launch_keys(pk, k, ktab, d->kscr.p, s));
   HIP_OK(hipStreamSynchronize(s));
   return PV_OK;
 }

@@ -10,6 +10,7 @@ namespace pv {
 // base-point table: 129 niels entries (k*B, k = 0..128), 32 words each
 constexpr int BTAB_ENTRIES = 129;
 constexpr int BTAB_WORDS = 32;
+constexpr int BTAB_QUARTERS = 4;   // tables for 2^(64 q) B, q = 0..3 (comb kernel of prepared keys)
 // per-lane scratch: A table (9 cached entries k*(-A), 40 words each) + the
 // CURVE_K points awaiting the shared inversion (40 words each)
 constexpr int ATAB_WORDS = 9 * 40 + 4 * 40;
@@ -24,7 +25,7 @@ struct DeviceCaps {
 hipError_t launch_btable_init(uint32_t* btab, hipStream_t s);
 
 // resident curve-kernel blocks per CU (occupancy query)
-hipError_t curve_occupancy(int* blocks_per_cu);
+hipError_t curve_occupancy(int* blocks_per_cu, bool keyed = false);
 
 // pre[i] = 1 iff S canonical, R/A not small order, A canonical;
 // dig[i] (16 words) = SHA-512(R||A||M) when pre[i] (reduced mod L by the curve
@@ -44,9 +45,11 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab = nullptr,
                         const uint32_t* kidx = nullptr);
 
-// prepared keys: KEY_WORDS words per key (table of k*(-A) + status)
-constexpr int KEYTAB_WORDS = 9 * 40 + 8;
-hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, hipStream_t s);
+// prepared keys: KEYTAB_WORDS words per key (4 comb tables of affine multiples
+// k * 2^(64 q) * (-A) + status); KEYTAB_SCRATCH words of scratch per key
+constexpr int KEYTAB_WORDS = 4 * 9 * 32 + 8;
+constexpr int KEYTAB_SCRATCH = 32 * 10;
+hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
 
 // keygen + sign: pk[i], sig[i] for seed[i] over M_i
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n,

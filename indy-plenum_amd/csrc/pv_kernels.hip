@@ -25,7 +25,8 @@ namespace pv {
 #endif
 
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
-                  KEY_WORDS == KEYTAB_WORDS, "table layout");
+                  KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && COMB_Q == BTAB_QUARTERS,
+              "table layout");
 
 // ------------------------------------------------------------- hash kernel
 // Persistent lanes with per-lane refill: each lane runs ONE SHA-512
@@ -108,13 +109,15 @@ hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blo
 }
 
 // ---------------------------------------------------------- base-point table
+// BTAB_QUARTERS tables, q-major: entry k of table q = k * 2^(64 q) * B
 __global__ void k_btable_init(uint32_t* btab) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < BTAB_ENTRIES) btable_entry(btab + k * BTAB_WORDS, k);
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < BTAB_QUARTERS * BTAB_ENTRIES) btable_entry(btab + g * BTAB_WORDS, g % BTAB_ENTRIES, g / BTAB_ENTRIES);
 }
 
 hipError_t launch_btable_init(uint32_t* btab, hipStream_t s) {
-  hipLaunchKernelGGL(k_btable_init, dim3(3), dim3(64), 0, s, btab);
+  const int n = BTAB_QUARTERS * BTAB_ENTRIES;
+  hipLaunchKernelGGL(k_btable_init, dim3((n + 63) / 64), dim3(64), 0, s, btab);
   return hipGetLastError();
 }
 
@@ -134,15 +137,16 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
                                                                         uint64_t* __restrict__ bitmap, uint64_t n,
                                                                         const uint32_t* __restrict__ ktab,
                                                                         const uint32_t* __restrict__ kidx) {
-  __shared__ uint32_t btab[BTAB_ENTRIES * BTAB_WORDS];
-  for (int j = threadIdx.x; j < BTAB_ENTRIES * BTAB_WORDS; j += CURVE_BLOCK) btab[j] = btab_g[j];
+  // generic kernel: table q = 0 (16.5 KB); comb kernel of prepared keys: all 4 (66 KB)
+  constexpr int BT_LDS_WORDS = (KEYED ? BTAB_QUARTERS : 1) * BTAB_ENTRIES * BTAB_WORDS;
+  __shared__ uint32_t btab[BT_LDS_WORDS];
+  for (int j = threadIdx.x; j < BT_LDS_WORDS; j += CURVE_BLOCK) btab[j] = btab_g[j];
   __syncthreads();
   const uint64_t nthreads = (uint64_t)gridDim.x * CURVE_BLOCK;
   const uint64_t gid = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
   uint32_t* lane = scratch + gid * LANE_WORDS;
   for (uint64_t base = 0; base < n; base += CURVE_K * nthreads) {
-    const uint32_t okm = KEYED ? curve_group(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx)
-                               : curve_group(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab);
+    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx);
 #pragma unroll
     for (int k = 0; k < CURVE_K; ++k) {
       const uint64_t i = base + (uint64_t)k * nthreads + gid;
@@ -156,9 +160,13 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
   }
 }
 
-hipError_t curve_occupancy(int* blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_curve<false>),
-                                                      CURVE_BLOCK, 0);
+hipError_t curve_occupancy(int* blocks_per_cu, bool keyed) {
+  return keyed ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu,
+                                                              reinterpret_cast<const void*>(k_curve<true>),
+                                                              CURVE_BLOCK, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu,
+                                                              reinterpret_cast<const void*>(k_curve<false>),
+                                                              CURVE_BLOCK, 0);
 }
 
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
@@ -180,14 +188,15 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
 }
 
 // -------------------------------------------------------------- key cache
-__global__ __launch_bounds__(256) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab) {
+__global__ __launch_bounds__(256) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
+                                               uint32_t* __restrict__ scr) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j < k) key_prepare(ktab + j * KEY_WORDS, pk + 32 * j);
+  if (j < k) key_prepare(ktab + j * KEY_WORDS, scr + j * KEY_SCRATCH, pk + 32 * j);
 }
 
-hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, hipStream_t s) {
+hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s) {
   if (k == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_keys, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, s, pk, k, ktab);
+  hipLaunchKernelGGL(k_keys, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, s, pk, k, ktab, scr);
   return hipGetLastError();
 }
 

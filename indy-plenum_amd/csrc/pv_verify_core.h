@@ -218,10 +218,18 @@ PV_HD void ge_basepoint(ge_p3& B) {
   fe_neg(B.T, nb.T); fe_carry(B.T);
 }
 
-// niels form of k*B (k <= 255), written as 32 words
-PV_HD void btable_entry(uint32_t* p, int k) {
+// niels form of k * 2^(64 q) * B (k <= 255, q = 0..3), written as 32 words.
+// Table q = 0 serves the generic kernel; the comb kernel of prepared keys uses
+// all four (B_q = 2^(64 q) B, so S*B = sum_q S_q B_q with 64-bit S_q).
+PV_HD void btable_entry(uint32_t* p, int k, int q = 0) {
   ge_p3 B, acc;
   ge_basepoint(B);
+#pragma unroll 1
+  for (int d = 0; d < 64 * q; ++d) {
+    ge_p1p1 t;
+    ge_p3_dbl(t, B);
+    ge_p1p1_to_p3(B, t);
+  }
   ge_cached cb;
   ge_p3_to_cached(cb, B);
   ge_p3_0(acc);
@@ -398,32 +406,170 @@ PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const u
 }
 
 // ------------------------------------------------------------- key cache
-// One verifying key, prepared once and shared by every signature under it:
-// the 9-entry table of cached multiples k*(-A) (AT_WORDS) and a status word
-// (1 = A canonical, not small order, decompresses; SURVEY.md App. C.2 steps
-// 2-4).  KEY_WORDS per key in HBM.
-constexpr int KEY_STATUS = AT_WORDS;
-constexpr int KEY_WORDS = AT_WORDS + 8;
+// A verifying key prepared once and shared by every signature under it, as a
+// 4-way comb: A_q = 2^(64 q) * (-A) for q = 0..3, each with its 9 multiples
+// k * A_q (k = 0..8) in AFFINE niels form (y+x, y-x, 2dxy; 32 words per entry,
+// all 32 non-trivial points normalised with one shared inversion).  Then
+//   h*(-A) = sum_q h_q A_q,   S*B = sum_q S_q B_q   (h_q, S_q the 64-bit quarters)
+// and the double-scalar multiplication needs 60 doublings instead of 256.  The
+// group element R' = h(-A) + S B is the same, so the verdict (encode(R') == R)
+// is bit-identical.  Status word: 1 = A canonical,
+// not small order, decompresses (steps 2-4).
+constexpr int COMB_Q = 4;
+constexpr int KT_ENTRY = 32;
+constexpr int KT_TABLE = 9 * KT_ENTRY;
+constexpr int KEY_STATUS = COMB_Q * KT_TABLE;
+constexpr int KEY_WORDS = KEY_STATUS + 8;
+constexpr int KEY_SCRATCH = 32 * 10;   // prefix products of the shared inversion
 
-PV_HD void key_prepare(uint32_t* kt, const uint8_t* pk) {
-  uint32_t A[8];
-  load8(A, pk);
-  ge_p3 negA;
-  bool ok = y_is_canonical(A) && !has_small_order(A) && ge_frombytes_negate(negA, A);
-  if (ok) {
-    build_atab(kt, negA);
-  } else {
-#pragma unroll 1
-    for (int k = 0; k < AT_WORDS; ++k) kt[k] = 0;
-  }
-#pragma unroll
-  for (int k = AT_WORDS; k < KEY_WORDS; ++k) kt[k] = 0;
-  kt[KEY_STATUS] = ok ? 1u : 0u;
+PV_HD void store_xyz(uint32_t* p, const ge_p3& q) {
+  store_fe(p, q.X);
+  store_fe(p + 10, q.Y);
+  store_fe(p + 20, q.Z);
 }
 
-// R' = h(-A) + S B with -A's table taken from a prepared key
+// kt: KEY_WORDS words; scr: KEY_SCRATCH words of per-key scratch
+PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
+  uint32_t A[8];
+  load8(A, pk);
+  ge_p3 P;
+  const bool ok = y_is_canonical(A) && !has_small_order(A) && ge_frombytes_negate(P, A);
+#pragma unroll 1
+  for (int k = 0; k < KEY_WORDS; ++k) kt[k] = 0;
+  kt[KEY_STATUS] = ok ? 1u : 0u;
+  if (!ok) return;
+  // projective multiples k * A_q (X, Y, Z) into the entry slots
+#pragma unroll 1
+  for (int q = 0; q < COMB_Q; ++q) {
+    uint32_t* tq = kt + q * KT_TABLE;
+    ge_cached c1;
+    ge_p3_to_cached(c1, P);
+    ge_p3 Q = P;
+    store_xyz(tq + KT_ENTRY, Q);
+#pragma unroll 1
+    for (int k = 2; k <= 8; ++k) {
+      ge_p1p1 t;
+      ge_add_cached(t, Q, c1, false);
+      ge_p1p1_to_p3(Q, t);
+      store_xyz(tq + k * KT_ENTRY, Q);
+    }
+    if (q + 1 < COMB_Q) {  // A_{q+1} = 2^64 A_q = 2^61 (8 A_q)
+      ge_p1p1 t;
+      ge_p2 r;
+      fe_copy(r.X, Q.X);
+      fe_copy(r.Y, Q.Y);
+      fe_copy(r.Z, Q.Z);
+#pragma unroll 1
+      for (int d = 0; d < 60; ++d) {
+        ge_p2_dbl(t, r);
+        ge_p1p1_to_p2(r, t);
+      }
+      ge_p2_dbl(t, r);
+      ge_p1p1_to_p3(P, t);
+    }
+  }
+  // one inversion for all 32 Z's (Montgomery's trick; prefix products in scr)
+  fe acc, z, u;
+#pragma unroll 1
+  for (int e = 0; e < 32; ++e) {
+    const uint32_t* slot = kt + (e >> 3) * KT_TABLE + ((e & 7) + 1) * KT_ENTRY;
+    load_fe(z, slot + 20);
+    if (e == 0) fe_copy(acc, z);
+    else fe_mul(acc, acc, z);
+    store_fe(scr + 10 * e, acc);
+  }
+  fe_invert(acc, acc);
+  fe d2;
+  fe_const_d2(d2);
+#pragma unroll 1
+  for (int e = 31; e >= 0; --e) {
+    uint32_t* slot = kt + (e >> 3) * KT_TABLE + ((e & 7) + 1) * KT_ENTRY;
+    fe zi, x, y;
+    if (e > 0) {
+      load_fe(u, scr + 10 * (e - 1));
+      fe_mul(zi, acc, u);            // Z_e^-1
+      load_fe(z, slot + 20);
+      fe_mul(acc, acc, z);           // (Z_0 ... Z_{e-1})^-1
+    } else {
+      fe_copy(zi, acc);
+    }
+    load_fe(x, slot);
+    fe_mul(x, x, zi);
+    load_fe(y, slot + 10);
+    fe_mul(y, y, zi);
+    fe_add(u, y, x); fe_carry(u);
+    store_fe(slot, u);
+    fe_sub(u, y, x); fe_carry(u);
+    store_fe(slot + 10, u);
+    fe_mul(u, x, y);
+    fe_mul(u, u, d2);
+    store_fe(slot + 20, u);
+  }
+  // identity entries (k = 0): y+x = 1, y-x = 1, 2dxy = 0
+#pragma unroll 1
+  for (int q = 0; q < COMB_Q; ++q) {
+    kt[q * KT_TABLE] = 1;
+    kt[q * KT_TABLE + 10] = 1;
+  }
+}
+
+// R' = hh*(-A) + ss*B from a prepared key (4 comb tables in kt) and the four
+// base-point tables (btab4, q-major, BT_ENTRIES x BT_WORDS each).  Windows
+// w = 15..0 (4 doublings apart): per window one affine add per quarter with the
+// signed radix-16 digit 16q + w of hh, and on even windows one per quarter with
+// the signed radix-256 digit 8q + w/2 of ss.  Digit words: 2q + (w >> 3).
+PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32_t ss[8], const uint32_t* kt,
+                                  const uint32_t* btab4) {
+  uint32_t hp[8], sp[8];
+  sc_add_pattern(hp, hh, 0x88888888u);
+  sc_add_pattern(sp, ss, 0x80808080u);
+  ge_p3 acc;
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_p2 r2;
+#pragma unroll 1
+  for (int half = 1; half >= 0; --half) {
+    uint32_t hw[4], sw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      hw[q] = half ? hp[2 * q + 1] : hp[2 * q];
+      sw[q] = half ? sp[2 * q + 1] : sp[2 * q];
+    }
+#pragma unroll 1
+    for (int i = 7; i >= 0; --i) {
+      if (half == 0 || i != 7) {
+#pragma unroll 1
+        for (int k = 0; k < 3; ++k) {
+          ge_p2_dbl(t, r2);
+          ge_p1p1_to_p2(r2, t);
+        }
+        ge_p2_dbl(t, r2);
+        ge_p1p1_to_p3(acc, t);
+      }
+      const bool bwin = (i & 1) == 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dA = (int)((hw[q] >> (4 * i)) & 15u) - 8;
+        ge_madd_at(t, acc, kt + q * KT_TABLE + (dA < 0 ? -dA : dA) * KT_ENTRY, dA < 0);
+        if (q < 3 || bwin) ge_p1p1_to_p3(acc, t);
+      }
+      if (bwin) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int dB = (int)((sw[q] >> (8 * (i >> 1))) & 255u) - 128;
+          ge_madd_at(t, acc, btab4 + (q * BT_ENTRIES + (dB < 0 ? -dB : dB)) * BT_WORDS, dB < 0);
+          if (q < 3) ge_p1p1_to_p3(acc, t);
+        }
+      }
+      ge_p1p1_to_p2(r2, t);
+    }
+  }
+  out = r2;
+}
+
+// R' = h(-A) + S B with -A's comb tables taken from a prepared key
 PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, const uint32_t* dig_src,
-                             const uint32_t* btab) {
+                             const uint32_t* btab4) {
   if (!kt[KEY_STATUS]) return false;
   uint32_t hh[8], S[8];
   {
@@ -433,7 +579,7 @@ PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, 
     sc_reduce64(hh, dig);
   }
   load8(S, sig + 32);
-  double_scalarmult(rp, hh, S, kt, btab);
+  double_scalarmult_comb(rp, hh, S, kt, btab4);
   return true;
 }
 
@@ -470,7 +616,9 @@ PV_HD void batch_invert_z(uint32_t* pts, int K) {
 // One lane's group of CURVE_K signatures i0, i0 + stride, ...: returns the
 // accepted bitmask.  Rejected or absent entries carry Z = 1 through the
 // shared inversion.  scratch = LANE_WORDS words owned by this lane.
-// Keyed mode (ktab != nullptr): signature i uses prepared key kidx[i].
+// KEYED: signature i uses prepared key kidx[i] (comb tables in ktab; btab
+// then holds the four quarter tables).
+template <bool KEYED>
 PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre, uint64_t i0,
                            uint64_t stride, uint64_t n, uint32_t* scratch, const uint32_t* btab,
                            const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
@@ -482,7 +630,7 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     ge_p2 rp;
     bool ok = false;
     if (i < n && pre[i]) {
-      if (ktab)
+      if constexpr (KEYED)
         ok = curve_point_keyed(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, btab);
       else
         ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);

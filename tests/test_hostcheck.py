@@ -141,7 +141,7 @@ def test_op_counts_pin_bench_constants(hc):
     blob = np.frombuffer(os.urandom(256 * n), np.uint8)
     off = np.arange(n + 1, dtype=np.uint64) * 256
     pk, sig = orc.sign_batch(seeds, blob, off)
-    hc.hc_btable((ctypes.c_uint32 * (129 * 32))())  # base-point table outside the counted region
+    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())  # base-point table outside the counted region
     hc.hc_reset_counts()
     assert hc_verify(hc, pk, sig, blob, off).all()
     c, bad = counts(hc)
@@ -214,7 +214,7 @@ def test_keyed_path_adversarial_bit_exact(hc, adversarial):
 
 
 def test_op_counts_pin_keyed_constants(hc):
-    """Work split of the prepared-key path (bench.py W_*_KEYED / W_*_KEYPREP):
+    """Work split of the prepared-key (comb) path (bench.py W_*_KEYED / W_*_KEYPREP):
     16 signatures under ONE prepared key vs 16 keys prepared."""
     import bench
     n = 16
@@ -222,7 +222,7 @@ def test_op_counts_pin_keyed_constants(hc):
     blob = np.frombuffer(os.urandom(256 * n), np.uint8)
     off = np.arange(n + 1, dtype=np.uint64) * 256
     pk, sig = orc.sign_batch(seeds, blob, off)
-    hc.hc_btable((ctypes.c_uint32 * (129 * 32))())
+    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())
     v = np.zeros(n, np.uint8)
 
     def run(upk, kidx, s, b):
@@ -240,6 +240,7 @@ def test_op_counts_pin_keyed_constants(hc):
     prep_sq = (int(c_many[1]) - int(c_one[1])) / (n - 1)
     assert prep_sq == bench.W_SQ_KEYPREP
     assert (int(c_one[1]) - prep_sq) / n == bench.W_SQ_KEYED
+    # the decompression multiplies by sqrt(-1) for about half of all keys
     prep_mul = (int(c_many[0]) - int(c_one[0])) / (n - 1)
-    assert abs(prep_mul - bench.W_MUL_KEYPREP) <= 0.5
-    assert abs((int(c_one[0]) - prep_mul) / n - bench.W_MUL_KEYED) <= 0.1
+    assert abs(prep_mul - bench.W_MUL_KEYPREP) <= 1.0
+    assert abs((int(c_one[0]) - prep_mul) / n - bench.W_MUL_KEYED) <= 0.2

@@ -56,12 +56,13 @@ static void hc_check_sq(const uint32_t* f) {
 
 using namespace pv;
 
-static uint32_t g_btab[BT_ENTRIES * BT_WORDS];
+static uint32_t g_btab[COMB_Q * BT_ENTRIES * BT_WORDS];
 static int g_btab_ready = 0;
 
 static void ensure_btab() {
   if (g_btab_ready) return;
-  for (int k = 0; k < BT_ENTRIES; ++k) btable_entry(g_btab + k * BT_WORDS, k);
+  for (int q = 0; q < COMB_Q; ++q)
+    for (int k = 0; k < BT_ENTRIES; ++k) btable_entry(g_btab + (q * BT_ENTRIES + k) * BT_WORDS, k, q);
   g_btab_ready = 1;
 }
 
@@ -78,7 +79,7 @@ void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
   for (uint64_t i = 0; i < n; ++i)
     pre[i] = hash_one(h + 16 * i, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
   for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
-    const uint32_t okm = curve_group(pk, sig, h, pre, i0, 1, n, lane, g_btab);
+    const uint32_t okm = curve_group<false>(pk, sig, h, pre, i0, 1, n, lane, g_btab);
     for (int k = 0; k < CURVE_K && i0 + k < n; ++k) verdict[i0 + k] = (okm >> k) & 1u;
   }
   free(h);
@@ -91,13 +92,15 @@ void hc_verify_keyed(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const 
   ensure_btab();
   static uint32_t lane[LANE_WORDS];
   uint32_t* ktab = (uint32_t*)calloc(k ? k * KEY_WORDS : KEY_WORDS, sizeof(uint32_t));
-  for (uint64_t j = 0; j < k; ++j) key_prepare(ktab + j * KEY_WORDS, pk + 32 * j);
+  uint32_t* scr = (uint32_t*)calloc(KEY_SCRATCH, sizeof(uint32_t));
+  for (uint64_t j = 0; j < k; ++j) key_prepare(ktab + j * KEY_WORDS, scr, pk + 32 * j);
+  free(scr);
   uint32_t* h = (uint32_t*)calloc(n ? n * 16 : 16, sizeof(uint32_t));
   uint8_t* pre = (uint8_t*)calloc(n ? n : 1, 1);
   for (uint64_t i = 0; i < n; ++i)
     pre[i] = hash_one(h + 16 * i, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
   for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
-    const uint32_t okm = curve_group(pk, sig, h, pre, i0, 1, n, lane, g_btab, ktab, kidx);
+    const uint32_t okm = curve_group<true>(pk, sig, h, pre, i0, 1, n, lane, g_btab, ktab, kidx);
     for (int q = 0; q < CURVE_K && i0 + q < n; ++q) verdict[i0 + q] = (okm >> q) & 1u;
   }
   free(ktab);
