@@ -11,9 +11,11 @@
 
 namespace pv {
 
-PV_HD uint64_t sha_k(int i) {
-  // first 64 bits of the fractional parts of the cube roots of the first 80 primes
-  const uint64_t K[80] = {
+// first 64 bits of the fractional parts of the cube roots of the first 80
+// primes; device copy in constant memory (read with scalar loads: the round
+// index is wave-uniform)
+#if defined(__HIPCC__)
+__constant__ uint64_t PV_SHA512_K[80] = {
       0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
       0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
       0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
@@ -34,9 +36,31 @@ PV_HD uint64_t sha_k(int i) {
       0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
       0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
       0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull,
-  };
-  return K[i];
-}
+};
+#else
+static const uint64_t PV_SHA512_K[80] = {
+      0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
+      0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
+      0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
+      0x72be5d74f27b896full, 0x80deb1fe3b1696b1ull, 0x9bdc06a725c71235ull, 0xc19bf174cf692694ull,
+      0xe49b69c19ef14ad2ull, 0xefbe4786384f25e3ull, 0x0fc19dc68b8cd5b5ull, 0x240ca1cc77ac9c65ull,
+      0x2de92c6f592b0275ull, 0x4a7484aa6ea6e483ull, 0x5cb0a9dcbd41fbd4ull, 0x76f988da831153b5ull,
+      0x983e5152ee66dfabull, 0xa831c66d2db43210ull, 0xb00327c898fb213full, 0xbf597fc7beef0ee4ull,
+      0xc6e00bf33da88fc2ull, 0xd5a79147930aa725ull, 0x06ca6351e003826full, 0x142929670a0e6e70ull,
+      0x27b70a8546d22ffcull, 0x2e1b21385c26c926ull, 0x4d2c6dfc5ac42aedull, 0x53380d139d95b3dfull,
+      0x650a73548baf63deull, 0x766a0abb3c77b2a8ull, 0x81c2c92e47edaee6ull, 0x92722c851482353bull,
+      0xa2bfe8a14cf10364ull, 0xa81a664bbc423001ull, 0xc24b8b70d0f89791ull, 0xc76c51a30654be30ull,
+      0xd192e819d6ef5218ull, 0xd69906245565a910ull, 0xf40e35855771202aull, 0x106aa07032bbd1b8ull,
+      0x19a4c116b8d2d0c8ull, 0x1e376c085141ab53ull, 0x2748774cdf8eeb99ull, 0x34b0bcb5e19b48a8ull,
+      0x391c0cb3c5c95a63ull, 0x4ed8aa4ae3418acbull, 0x5b9cca4f7763e373ull, 0x682e6ff3d6b2b8a3ull,
+      0x748f82ee5defb2fcull, 0x78a5636f43172f60ull, 0x84c87814a1f0ab72ull, 0x8cc702081a6439ecull,
+      0x90befffa23631e28ull, 0xa4506cebde82bde9ull, 0xbef9a3f7b2c67915ull, 0xc67178f2e372532bull,
+      0xca273eceea26619cull, 0xd186b8c721c0c207ull, 0xeada7dd6cde0eb1eull, 0xf57d4f7fee6ed178ull,
+      0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
+      0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
+      0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull,
+};
+#endif
 
 PV_HD void sha512_init(uint64_t h[8]) {
   h[0] = 0x6a09e667f3bcc908ull; h[1] = 0xbb67ae8584caa73bull;
@@ -45,32 +69,81 @@ PV_HD void sha512_init(uint64_t h[8]) {
   h[6] = 0x1f83d9abfb41bd6bull; h[7] = 0x5be0cd19137e2179ull;
 }
 
-PV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate / shift on the two 32-bit halves: one v_alignbit_b32 per half
+// (n is a compile-time constant in the unrolled rounds, so the branch folds)
+PV_HD uint64_t rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rl, rh;
+  if (n < 32) {
+    rl = __builtin_amdgcn_alignbit(hi, lo, n);
+    rh = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rl = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rh = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rh << 32) | rl;
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+
+PV_HD uint64_t shr64(uint64_t x, int n) {  // n < 32
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return x >> n;
+#endif
+}
+
+// 3-input bitwise functions on both halves: one v_bitop3_b32 per half on
+// gfx950 (truth tables in the f(0xf0, 0xcc, 0xaa) convention: xor3 0x96,
+// choose 0xca, majority 0xe8)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PV_BITOP3_64(a, b, c, T)                                                                        \
+  ((((uint64_t)(uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)((a) >> 32), (uint32_t)((b) >> 32),     \
+                                                     (uint32_t)((c) >> 32), (T)))                       \
+    << 32) |                                                                                            \
+   (uint64_t)(uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(a), (uint32_t)(b), (uint32_t)(c), (T)))
+PV_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) { return PV_BITOP3_64(a, b, c, 0x96); }
+PV_HD uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) { return PV_BITOP3_64(e, f, g, 0xca); }
+PV_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return PV_BITOP3_64(a, b, c, 0xe8); }
+#else
+PV_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) { return a ^ b ^ c; }
+PV_HD uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) { return (e & f) | (~e & g); }
+PV_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return (a & b) | (a & c) | (b & c); }
+#endif
 
 // one compression; w[16] holds the block as big-endian-decoded 64-bit words
-// (it is overwritten by the schedule).
+// (it is overwritten by the schedule).  Per round: 6 alignbit + 2 bitop3 per
+// Sigma, 2 bitop3 for Ch, 2 for Maj, 7 64-bit adds.
+PV_HD void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e, uint64_t& f, uint64_t& g,
+                        uint64_t& k, uint64_t kw) {
+  const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+  const uint64_t t1 = k + S1 + ch64(e, f, g) + kw;
+  const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+  const uint64_t t2 = S0 + maj64(a, b, c);
+  k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+}
+
 PV_HD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
   PV_COUNT(sha);
   uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
-#pragma unroll
-  for (int i = 0; i < 80; ++i) {
-    uint64_t wi;
-    if (i < 16) {
-      wi = w[i];
-    } else {
-      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
+#pragma clang loop unroll(full)
+  for (int j = 0; j < 16; ++j) sha512_round(a, b, c, d, e, f, g, k, PV_SHA512_K[j] + w[j]);
+  // rounds 16..79: 4 passes of 16 with the rolling schedule at static indices
+  // (kept as a loop: the fully unrolled 80 rounds overflow the instruction cache)
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
+#pragma clang loop unroll(full)
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
+      w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+      sha512_round(a, b, c, d, e, f, g, k, PV_SHA512_K[r + j] + w[j]);
     }
-    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = k + S1 + ch + sha_k(i) + wi;
-    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-    const uint64_t t2 = S0 + mj;
-    k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
 }

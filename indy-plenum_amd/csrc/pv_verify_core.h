@@ -113,18 +113,27 @@ PV_HD uint32_t funnel32(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 
-// 32 little-endian words = message bytes [q, q + 128) with SHA padding
-// applied: bytes past mlen are zero and byte mlen is 0x80.  One guarded
-// aligned load per word that holds a message byte, then a funnel shift: the
-// blob only needs the usual 16 readable bytes after the last message.
-PV_HD void msg_window(uint32_t x[32], const uint8_t* m, uint64_t mlen, uint64_t q) {
+// message byte offset of block `blk` of R || A || M (block 0 holds R || A and M[0, 64))
+PV_HD uint64_t hram_q(uint64_t blk) { return blk == 0 ? 0 : 128 * blk - 64; }
+
+// Raw aligned words covering message bytes [q, q + 128): one guarded load per
+// word that holds a message byte (the blob only needs the usual 16 readable
+// bytes after the last message).  Split from the assembly so the hash kernel
+// can issue the next block's loads before compressing the current one.
+PV_HD void msg_fetch(uint32_t y[33], const uint8_t* m, uint64_t mlen, uint64_t q) {
   const int64_t rem = (int64_t)mlen - (int64_t)q;
   const uintptr_t base = reinterpret_cast<uintptr_t>(m) + q;
   const uint32_t mis = (uint32_t)(base & 3u);
   const uint32_t* wp = reinterpret_cast<const uint32_t*>(base - mis);
-  uint32_t y[33];
 #pragma unroll
   for (int k = 0; k < 33; ++k) y[k] = (int64_t)(4 * k) - (int64_t)mis < rem ? wp[k] : 0u;
+}
+
+// 32 little-endian words = message bytes [q, q + 128) with SHA padding applied:
+// bytes past mlen are zero and byte mlen is 0x80 (funnel shift of the raw words)
+PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[33], const uint8_t* m, uint64_t mlen, uint64_t q) {
+  const int64_t rem = (int64_t)mlen - (int64_t)q;
+  const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + q) & 3u);
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     uint32_t v = funnel32(y[k + 1], y[k], 8u * mis);
@@ -137,13 +146,13 @@ PV_HD void msg_window(uint32_t x[32], const uint8_t* m, uint64_t mlen, uint64_t 
   }
 }
 
-// block `blk` of R || A || M as 16 big-endian 64-bit words (R, A read from
-// sig/pk on block 0; length words on the last block)
-PV_HD void hram_block(uint64_t w[16], const uint8_t* sig, const uint8_t* pk, const uint8_t* m, uint64_t mlen,
-                      uint64_t blk, uint64_t nblk) {
+// block `blk` of R || A || M as 16 big-endian 64-bit words from the raw message
+// words of hram_q(blk) (R, A read from sig/pk on block 0; length words on the last)
+PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[33], const uint8_t* sig, const uint8_t* pk,
+                         const uint8_t* m, uint64_t mlen, uint64_t blk, uint64_t nblk) {
   const bool first = blk == 0;
   uint32_t x[32];
-  msg_window(x, m, mlen, first ? 0 : 128 * blk - 64);
+  msg_assemble(x, y, m, mlen, hram_q(blk));
   if (first) {
     uint32_t ra[16];
     load8(ra, sig);
@@ -161,6 +170,13 @@ PV_HD void hram_block(uint64_t w[16], const uint8_t* sig, const uint8_t* pk, con
     w[14] = 0;
     w[15] = (64 + mlen) * 8;
   }
+}
+
+PV_HD void hram_block(uint64_t w[16], const uint8_t* sig, const uint8_t* pk, const uint8_t* m, uint64_t mlen,
+                      uint64_t blk, uint64_t nblk) {
+  uint32_t y[33];
+  msg_fetch(y, m, mlen, hram_q(blk));
+  hram_assemble(w, y, sig, pk, m, mlen, blk, nblk);
 }
 
 // pre-checks + digest = SHA-512(R||A||M) as 16 LE words (reduced mod L by the

@@ -35,12 +35,20 @@ KERNEL(mad_u64_u32, uint64_t, (uint64_t)(a + c),
        { uint64_t cc; asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[c]), "=s"(cc) : "v"(a), "v"(b)); })
 KERNEL(add_u32, uint32_t, a + c, { asm volatile("v_add_u32 %0, %0, %1" : "+v"(acc[c]) : "v"(b)); })
 KERNEL(lshrrev_b64, uint64_t, (uint64_t)(a + c), { asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(acc[c])); })
+KERNEL(alignbit_b32, uint32_t, a + c, { asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(acc[c]) : "v"(b)); })
+KERNEL(bitop3_b32, uint32_t, a + c,
+       { asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc[c]) : "v"(a), "v"(b)); })
+KERNEL(xor_b32, uint32_t, a + c, { asm volatile("v_xor_b32 %0, %0, %1" : "+v"(acc[c]) : "v"(b)); })
+KERNEL(lshl_add_u64, uint64_t, (uint64_t)(a + c),
+       { asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[c]) : "v"((uint64_t)b)); })
 
 typedef void (*kfn)(uint64_t*, uint32_t*, uint32_t, int);
 
 int main() {
   struct { const char* name; kfn f; } ks[] = {
-      {"v_mad_u64_u32", k_mad_u64_u32}, {"v_add_u32", k_add_u32}, {"v_lshrrev_b64", k_lshrrev_b64}};
+      {"v_mad_u64_u32", k_mad_u64_u32}, {"v_add_u32", k_add_u32}, {"v_lshrrev_b64", k_lshrrev_b64},
+      {"v_alignbit_b32", k_alignbit_b32}, {"v_bitop3_b32", k_bitop3_b32}, {"v_xor_b32", k_xor_b32},
+      {"v_lshl_add_u64", k_lshl_add_u64}};
   int cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, 0) == hipSuccess) cus = prop.multiProcessorCount;
