@@ -235,12 +235,83 @@ def main_c1(args):
     return 0 if mism == 0 else 3
 
 
+def main_f3(args):
+    """Row f3: ledger Merkle tree hash (leaf SHA-256 + RFC 6962 levels) of 1M x 256 B
+    leaves resident in HBM, vs the same tree hash with hashlib on one host thread."""
+    import hashlib
+    from plenum_gpu.device import _p, _stream
+    n = args.n or (1 << 20)
+    ln = 256
+    torch.cuda.set_device(0)
+    dev = torch.device('cuda', 0)
+    nat.ensure_init(1)
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    blob = torch.zeros(n * ln + 16, dtype=torch.uint8, device=dev)
+    blob[:n * ln] = torch.randint(0, 256, (n * ln,), dtype=torch.uint8, device=dev, generator=g)
+    off = torch.arange(n + 1, dtype=torch.int64, device=dev) * ln
+    leaves = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    root = torch.zeros(32, dtype=torch.uint8, device=dev)
+    lib = nat.load()
+
+    def step():
+        nat._check('pv_merkle_root_device', lib.pv_merkle_root_device(_p(blob), _p(off), n, _p(leaves), _p(root), 0,
+                                                                      _stream(dev)))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # check: root of the same leaves with hashlib (level-wise RFC 6962)
+    host = blob[:n * ln].cpu().numpy()
+    lvl = [hashlib.sha256(b'\x00' + host[i * ln:(i + 1) * ln].tobytes()).digest() for i in range(n)]
+    t1 = time.perf_counter()
+    while len(lvl) > 1:
+        nxt = [hashlib.sha256(b'\x01' + lvl[i] + lvl[i + 1]).digest() for i in range(0, len(lvl) - 1, 2)]
+        if len(lvl) % 2:
+            nxt.append(lvl[-1])
+        lvl = nxt
+    mism = int(bytes(root.cpu().numpy()) != lvl[0])
+    # CPU baseline: the same tree hash on one host thread over a bounded sample
+    sample = min(n, 1 << 17)
+    t0 = time.perf_counter()
+    lv = [hashlib.sha256(b'\x00' + host[i * ln:(i + 1) * ln].tobytes()).digest() for i in range(sample)]
+    while len(lv) > 1:
+        nx = [hashlib.sha256(b'\x01' + lv[i] + lv[i + 1]).digest() for i in range(0, len(lv) - 1, 2)]
+        if len(lv) % 2:
+            nx.append(lv[-1])
+        lv = nx
+    cpu_rate = sample / (time.perf_counter() - t0)
+    del t1
+    value = n * args.steps / elapsed
+    res = {
+        'metric': 'Merkle tree hash leaves/sec (ledger TreeHasher.hash_full_tree, SHA-256)', 'value': round(value, 1),
+        'unit': 'leaves/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic random leaves resident in HBM',
+        'config': {'workload': 'SURVEY.md 8(f) f3: Merkle tree hash of 1M x 256 B ledger leaves (leaf digests + '
+                               'RFC 6962 levels), one GPU', 'name': 'f3', 'leaves': n, 'leaf_bytes': ln},
+        'verdict_mismatches': mism,
+        'input_gbps': round(n * ln * args.steps / elapsed / 1e9, 2),
+        'roofline': None,
+        'cpu_baseline': {'value': round(cpu_rate, 1), 'unit': 'leaves/s', 'cores': 1, 'kind': 'port',
+                         'sample': 'hashlib SHA-256 tree hash (the reference TreeHasher algorithm, level-wise) over '
+                                   'the first {} leaves on 1 host thread'.format(sample)},
+    }
+    print(json.dumps(res), flush=True)
+    return 0 if mism == 0 else 3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=sorted(CONFIGS), default='c2', help='workload (default c2, the headline)')
+    ap.add_argument('--config', choices=sorted(CONFIGS) + ['f3'], default='c2',
+                    help='workload (default c2, the headline; f3 = ledger Merkle hashing)')
     ap.add_argument('--n', type=int, default=None, help='signatures per GPU (default: the config\'s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-key-cache', action='store_true',
@@ -248,6 +319,8 @@ def main():
     args = ap.parse_args()
     if args.config == 'c1':
         return main_c1(args)
+    if args.config == 'f3':
+        return main_f3(args)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))

@@ -115,6 +115,25 @@ int pv_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, const 
                            const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n, uint8_t *verdict,
                            uint64_t *bitmap, int device, void *stream);
 
+/* SHA-256 / Merkle tree hashing.
+ *   pv_sha256_batch[_device]  digests[i] (32 bytes) = SHA-256(prefix || M_i); prefix -1 = none,
+ *                             0..255 = that single byte.  Replaces the per-request
+ *                             sha256(...).hexdigest() of Request.key / payload_digest
+ *                             (plenum/common/request.py:82-90).
+ *   pv_merkle_root[_device]   RFC 6962 Merkle Tree Hash of the leaves M_0..M_{n-1}, bit-identical
+ *                             to ledger/tree_hasher.py TreeHasher.hash_full_tree (:55-86; leaf =
+ *                             SHA-256(0x00 || M), node = SHA-256(0x01 || l || r), n = 0 ->
+ *                             SHA-256("")); leaf_hashes (n x 32, may be NULL) receives the leaf
+ *                             digests (TreeHasher.hash_leaf, :21-24).
+ * Device variants: root is a 32-byte DEVICE buffer; the blob needs >= 16 readable bytes after
+ * the last message. */
+int pv_sha256_batch(const uint8_t *blob, const uint64_t *off, uint64_t n, int32_t prefix, uint8_t *digests);
+int pv_sha256_batch_device(const uint8_t *blob, const uint64_t *off, uint64_t n, int32_t prefix, uint8_t *digests,
+                           int device, void *stream);
+int pv_merkle_root(const uint8_t *blob, const uint64_t *off, uint64_t n, uint8_t *root, uint8_t *leaf_hashes);
+int pv_merkle_root_device(const uint8_t *blob, const uint64_t *off, uint64_t n, uint8_t *leaf_hashes, uint8_t *root,
+                          int device, void *stream);
+
 /* Per-batch quorum tally (HOST memory).
  *   verdict    n_msgs bytes (1 = vote counts)
  *   sender     n_msgs node indices (< n_nodes <= 1024)

@@ -82,6 +82,8 @@ struct Device {
   DevBuf<uint64_t> scan;      // block sums of the device prefix scan
   DevBuf<uint32_t> ktab, kidx;  // prepared keys + per-signature key index (deduplicated host batches)
   DevBuf<uint32_t> kscr;        // key-preparation scratch
+  DevBuf<uint32_t> mk0, mk1;    // Merkle level ping-pong / leaf digests
+  int sha256_blocks = 0;
   int curve_blocks_keyed = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
@@ -125,6 +127,9 @@ int init_device(Device& d) {
   if (kper < 1) kper = 1;
   if (kper > per_cu) kper = per_cu;
   d.curve_blocks_keyed = d.cu_count * kper;
+  int sper = 0;
+  HIP_OK(pv::sha256_occupancy(&sper));
+  d.sha256_blocks = d.cu_count * (sper < 1 ? 1 : sper);
   int hper = 0;
   HIP_OK(pv::hash_occupancy(&hper));
   if (hper < 1) hper = 1;
@@ -143,7 +148,7 @@ void release_device(Device& d) {
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.bitmap.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
-  d.ktab.release(); d.kidx.release(); d.kscr.release();
+  d.ktab.release(); d.kidx.release(); d.kscr.release(); d.mk0.release(); d.mk1.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -488,6 +493,131 @@ int pv_sign_batch(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t*
   HIP_OK(pv::launch_sign(d.tamper.p, d.blob.p, d.off.p, n, d.btab.p, d.pk.p, d.sig.p, d.stream));
   HIP_OK(hipMemcpyAsync(pk_out, d.pk.p, n * 32, hipMemcpyDeviceToHost, d.stream));
   HIP_OK(hipMemcpyAsync(sig_out, d.sig.p, n * 64, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipStreamSynchronize(d.stream));
+  return PV_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// leaf digests (n x 8 words) -> root (8 words) on stream s, all device memory
+int enqueue_merkle(Device& d, const uint8_t* blob, const uint64_t* off, uint64_t n, uint32_t* leaves, uint32_t* root,
+                   hipStream_t s) {
+  if (n == 0) {  // hash_empty(): SHA-256 of the empty string (ledger/tree_hasher.py:17-19)
+    static const uint32_t empty[8] = {0x42c4b0e3u, 0x141cfc98u, 0xc8f4fb9au, 0x24b96f99u,
+                                      0xe441ae27u, 0x4c939b64u, 0x1b9995a4u, 0x55b85278u};
+    HIP_OK(hipMemcpyAsync(root, empty, 32, hipMemcpyHostToDevice, s));
+    return PV_OK;
+  }
+  HIP_OK(pv::launch_sha256(blob, off, n, 1, 0x00, d.counter.p, leaves, d.sha256_blocks, s));
+  const uint32_t* in = leaves;
+  uint64_t m = n;
+  int which = 0;
+  while (m > 1) {
+    uint32_t* out = (m + 1) / 2 == 1 ? root : (which ? d.mk1.p : d.mk0.p);
+    HIP_OK(pv::launch_merkle_level(in, m, out, s));
+    in = out;
+    m = (m + 1) / 2;
+    which ^= 1;
+  }
+  if (n == 1) HIP_OK(hipMemcpyAsync(root, leaves, 32, hipMemcpyDeviceToDevice, s));
+  return PV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int pv_sha256_batch_device(const uint8_t* blob, const uint64_t* off, uint64_t n, int32_t prefix, uint8_t* digests,
+                           int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n == 0) return PV_OK;
+  if (!blob || !off || !digests) return fail(PV_EINVAL, "null device buffer");
+  if (prefix > 255) return fail(PV_EINVAL, "prefix must be -1 (none) or a byte value");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(pv::launch_sha256(blob, off, n, prefix < 0 ? 0 : 1, prefix < 0 ? 0 : (uint32_t)prefix, d->counter.p,
+                           reinterpret_cast<uint32_t*>(digests), d->sha256_blocks, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_merkle_root_device(const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* leaf_hashes, uint8_t* root,
+                          int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (!root || (n && (!blob || !off))) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  uint32_t* leaves = reinterpret_cast<uint32_t*>(leaf_hashes);
+  if (!leaves && n) {
+    HIP_OK(d->mk1.ensure((n + 1) / 2 * 8 + n * 8));
+    leaves = d->mk1.p + (n + 1) / 2 * 8;
+  }
+  HIP_OK(d->mk0.ensure((n + 1) / 2 * 8 + 8));
+  if (leaf_hashes) HIP_OK(d->mk1.ensure((n + 1) / 2 * 8 + 8));
+  int rc = enqueue_merkle(*d, blob, off, n, leaves, reinterpret_cast<uint32_t*>(root), s);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_merkle_root(const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* root, uint8_t* leaf_hashes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (!root || (n && (!off || (!blob && off[n] != off[0])))) return fail(PV_EINVAL, "null buffer");
+  for (uint64_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) return fail(PV_EINVAL, "off not monotone at %llu", (unsigned long long)i);
+  Device& d = g_devs[0];
+  HIP_OK(hipSetDevice(d.id));
+  const uint64_t b0 = n ? off[0] : 0, bytes = n ? off[n] - b0 : 0;
+  std::vector<uint64_t> offs(n + 1);
+  for (uint64_t k = 0; k <= n; ++k) offs[k] = n ? off[k] - b0 : 0;
+  HIP_OK(d.blob.ensure(bytes + 16));
+  HIP_OK(d.off.ensure(n + 1));
+  HIP_OK(d.mk0.ensure((n + 1) / 2 * 8 + 8));
+  HIP_OK(d.mk1.ensure((n + 1) / 2 * 8 + n * 8 + 8));
+  uint32_t* leaves = d.mk1.p + (n + 1) / 2 * 8;
+  uint32_t* droot = d.mk0.p + (n + 1) / 2 * 8;
+  if (bytes) HIP_OK(hipMemcpyAsync(d.blob.p, blob + b0, bytes, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.stream));
+  HIP_OK(hipMemcpyAsync(d.off.p, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, d.stream));
+  int rc = enqueue_merkle(d, d.blob.p, d.off.p, n, leaves, droot, d.stream);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(root, droot, 32, hipMemcpyDeviceToHost, d.stream));
+  if (leaf_hashes && n) HIP_OK(hipMemcpyAsync(leaf_hashes, leaves, n * 32, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipStreamSynchronize(d.stream));
+  return PV_OK;
+}
+
+int pv_sha256_batch(const uint8_t* blob, const uint64_t* off, uint64_t n, int32_t prefix, uint8_t* digests) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (n == 0) return PV_OK;
+  if (!off || !digests || (!blob && off[n] != off[0])) return fail(PV_EINVAL, "null buffer");
+  if (prefix > 255) return fail(PV_EINVAL, "prefix must be -1 (none) or a byte value");
+  for (uint64_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) return fail(PV_EINVAL, "off not monotone at %llu", (unsigned long long)i);
+  Device& d = g_devs[0];
+  HIP_OK(hipSetDevice(d.id));
+  const uint64_t b0 = off[0], bytes = off[n] - b0;
+  std::vector<uint64_t> offs(n + 1);
+  for (uint64_t k = 0; k <= n; ++k) offs[k] = off[k] - b0;
+  HIP_OK(d.blob.ensure(bytes + 16));
+  HIP_OK(d.off.ensure(n + 1));
+  HIP_OK(d.mk0.ensure(n * 8));
+  if (bytes) HIP_OK(hipMemcpyAsync(d.blob.p, blob + b0, bytes, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.stream));
+  HIP_OK(hipMemcpyAsync(d.off.p, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(pv::launch_sha256(d.blob.p, d.off.p, n, prefix < 0 ? 0 : 1, prefix < 0 ? 0 : (uint32_t)prefix, d.counter.p,
+                           d.mk0.p, d.sha256_blocks, d.stream));
+  HIP_OK(hipMemcpyAsync(digests, d.mk0.p, n * 32, hipMemcpyDeviceToHost, d.stream));
   HIP_OK(hipStreamSynchronize(d.stream));
   return PV_OK;
 }

@@ -60,6 +60,13 @@ hipError_t launch_tally(const uint8_t* verdict, const uint32_t* sender, const ui
                         uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t* votes,
                         uint8_t* reached, hipStream_t s);
 
+// SHA-256 / Merkle: out (n x 8 words) = SHA-256(prefix || M_i)
+// (plen 0 or 1 prefix bytes); one Merkle level m -> ceil(m/2) nodes
+hipError_t sha256_occupancy(int* blocks_per_cu);
+hipError_t launch_sha256(const uint8_t* blob, const uint64_t* off, uint64_t n, uint32_t plen, uint32_t prefix,
+                         unsigned long long* counter, uint32_t* out, int blocks, hipStream_t s);
+hipError_t launch_merkle_level(const uint32_t* in, uint64_t m, uint32_t* out, hipStream_t s);
+
 // deterministic synthetic workload; spec in plenum_gpu/synth.py.
 // mode 0 FIXED (len = mlen_min), 1 RANGE (len uniform in [mlen_min, mlen_max]),
 // 2 COMMIT (C3 3PC batches of n_nodes votes).

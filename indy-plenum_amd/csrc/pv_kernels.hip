@@ -13,6 +13,7 @@
 // per-signature algorithms live in pv_verify_core.h.
 #include <hip/hip_runtime.h>
 #include "pv_verify_core.h"
+#include "pv_sha256.h"
 #include "pv_kernels.h"
 
 namespace pv {
@@ -266,6 +267,80 @@ hipError_t launch_tally(const uint8_t* verdict, const uint32_t* sender, const ui
   hipLaunchKernelGGL(k_tally, dim3((uint32_t)blocks), dim3(256), 0, s, verdict, sender, batch_off, n_batches, n_nodes,
                      quorum, votes, reached);
   return hipGetLastError();
+}
+
+// ----------------------------------------------- SHA-256 / Merkle (row f3)
+// Batch SHA-256 of (prefix || M_i): persistent lanes with per-lane refill, the
+// same work-queue scheme as k_hash (ragged messages cost no divergence).
+__global__ __launch_bounds__(256) void k_sha256(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+                                                 uint64_t n, uint32_t plen, uint32_t prefix,
+                                                 unsigned long long* __restrict__ counter, uint32_t* __restrict__ out) {
+  uint64_t idx = take_index(counter);
+  uint64_t blk = 0, nblk = 0, mo = 0, ml = 0;
+  uint32_t hs[8];
+  while (true) {
+    if (blk == nblk && idx < n) {
+      mo = off[idx];
+      ml = off[idx + 1] - mo;
+      nblk = sha256_blocks(ml, plen);
+      blk = 0;
+      sha256_init(hs);
+    }
+    if (idx >= n) break;
+    uint32_t w[16];
+    sha256_block(w, blob + mo, ml, plen, prefix, blk, nblk);
+    sha256_compress(hs, w);
+    if (++blk == nblk) {
+      uint32_t* o = out + 8 * idx;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = bswap32_(hs[k]);
+      idx = take_index(counter);
+    }
+  }
+}
+
+hipError_t launch_sha256(const uint8_t* blob, const uint64_t* off, uint64_t n, uint32_t plen, uint32_t prefix,
+                         unsigned long long* counter, uint32_t* out, int blocks, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  const uint64_t need = (n + 255) / 256;
+  const uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
+  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)b), dim3(256), 0, s, blob, off, n, plen, prefix, counter, out);
+  return hipGetLastError();
+}
+
+// one Merkle level: out[i] = SHA-256(0x01 || in[2i] || in[2i+1]); an odd last
+// node moves up unchanged (== RFC 6962 / ledger/tree_hasher.py MTH split at
+// the largest power of two below n)
+__global__ __launch_bounds__(256) void k_merkle_level(const uint32_t* __restrict__ in, uint64_t m,
+                                                      uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t half = m / 2;
+  if (i < half) {
+    uint32_t lr[16], h[8];
+    const uint32_t* p = in + 16 * i;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lr[k] = p[k];
+    sha256_node(h, lr);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[8 * i + k] = h[k];
+  } else if (i == half && (m & 1)) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[8 * i + k] = in[8 * (m - 1) + k];
+  }
+}
+
+hipError_t launch_merkle_level(const uint32_t* in, uint64_t m, uint32_t* out, hipStream_t s) {
+  const uint64_t outs = (m + 1) / 2;
+  if (outs == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merkle_level, dim3((uint32_t)((outs + 255) / 256)), dim3(256), 0, s, in, m, out);
+  return hipGetLastError();
+}
+
+hipError_t sha256_occupancy(int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_sha256), 256,
+                                                      0);
 }
 
 // ------------------------------------------------------- synthetic workload

@@ -384,7 +384,11 @@ PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss
     ge_p2_dbl(t, r2);
     ge_p1p1_to_p3(acc, t);
     const int dA = (int)((hw >> (4 * (i & 7))) & 15u) - 8;
+#ifdef PV_EXPERIMENT_FIXED_ENTRY   // timing experiment only: wrong verdicts, measures the table-fetch cost
+    ge_add_cached_at(t, acc, atab + AT_ENTRY, dA < 0);
+#else
     ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
+#endif
     if ((i & 1) == 0) {
       const int dB = (int)((sw >> (8 * ((i >> 1) & 3))) & 255u) - 128;
       ge_p1p1_to_p3(acc, t);

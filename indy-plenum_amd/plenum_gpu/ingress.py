@@ -46,9 +46,8 @@ def idr_from_req_data(data: dict):
     return ','.join(sorted(sigs.keys())) if sigs else None
 
 
-def request_key(req: dict, plugin_fields: Iterable[str] = ()) -> str:
-    """Request(**req).key = sha256(serialize_msg_for_signing(signingState())).hexdigest()
-    (plenum/common/request.py:82-120)."""
+def signing_state(req: dict, plugin_fields: Iterable[str] = ()) -> dict:
+    """Request(**req).signingState() (plenum/common/request.py:95-120)."""
     state = {IDENTIFIER: idr_from_req_data(req), REQ_ID: req.get(REQ_ID), OPERATION: req.get(OPERATION)}
     for k in (PROTOCOL_VERSION, TAA_ACCEPTANCE, ENDORSER):
         if req.get(k) is not None:
@@ -61,7 +60,13 @@ def request_key(req: dict, plugin_fields: Iterable[str] = ()) -> str:
         val = req.get(nm)
         if val:
             state[nm] = val
-    return sha256(serialize_msg_for_signing(state)).hexdigest()
+    return state
+
+
+def request_key(req: dict, plugin_fields: Iterable[str] = ()) -> str:
+    """Request(**req).key = sha256(serialize_msg_for_signing(signingState())).hexdigest()
+    (plenum/common/request.py:82-90); plenum_gpu.merkle.request_digests batches it on the GPU."""
+    return sha256(serialize_msg_for_signing(signing_state(req, plugin_fields))).hexdigest()
 
 
 def is_client_request(msg) -> bool:

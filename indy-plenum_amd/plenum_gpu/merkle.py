@@ -1,0 +1,80 @@
+"""Batch SHA-256 and Merkle tree hashing on the GPU.
+
+* `sha256_batch(msgs, prefix=None)` -> list of 32-byte digests, one GPU pass
+  (pv_sha256_batch).  `request_digests(reqs)` gives every request's
+  `Request.key` (plenum/common/request.py:82-90) with the native serializer and
+  one GPU pass.
+* `GpuTreeHasher` mirrors ledger/tree_hasher.py `TreeHasher` (hash_empty,
+  hash_leaf, hash_children, hash_full_tree) with `hash_full_tree` and
+  `hash_leaves` computed on the GPU (pv_merkle_root): leaf = SHA-256(0x00 || data),
+  node = SHA-256(0x01 || left || right), RFC 6962 shape.
+
+Like the verify path there is no CPU fallback: the library and a GPU are required.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+
+
+def _pack(msgs):
+    msgs = [bytes(m) for m in msgs]
+    blob, off = nat.pack_messages(msgs)
+    return np.ascontiguousarray(blob, np.uint8), np.ascontiguousarray(off, np.uint64)
+
+
+def sha256_batch(msgs, prefix=None):
+    """[bytes] -> [32-byte digest of (prefix || m)]; prefix None or a byte value."""
+    nat.ensure_init()
+    n = len(msgs)
+    if n == 0:
+        return []
+    blob, off = _pack(msgs)
+    out = np.zeros((n, 32), np.uint8)
+    p = -1 if prefix is None else int(prefix)
+    nat._check('pv_sha256_batch', nat.load().pv_sha256_batch(nat._ptr(blob), nat._ptr(off), n, p, nat._ptr(out)))
+    return [out[i].tobytes() for i in range(n)]
+
+
+def request_digests(reqs, plugin_fields=()):
+    """Request(**r).key (sha256 hex of the signing state) for every request, one GPU pass."""
+    from .ingress import signing_state
+    from .serialization import serialize_msg_for_signing
+    return [d.hex() for d in sha256_batch([serialize_msg_for_signing(signing_state(r, plugin_fields)) for r in reqs])]
+
+
+def merkle_root(leaves, with_leaf_hashes=False):
+    """RFC 6962 Merkle Tree Hash of `leaves` (bytes each) on the GPU."""
+    nat.ensure_init()
+    n = len(leaves)
+    blob, off = _pack(leaves)
+    root = np.zeros(32, np.uint8)
+    lh = np.zeros((max(n, 1), 32), np.uint8) if with_leaf_hashes else None
+    nat._check('pv_merkle_root', nat.load().pv_merkle_root(nat._ptr(blob), nat._ptr(off), n, nat._ptr(root),
+                                                           nat._ptr(lh) if lh is not None else ctypes.c_void_p(0)))
+    if with_leaf_hashes:
+        return root.tobytes(), [lh[i].tobytes() for i in range(n)]
+    return root.tobytes()
+
+
+class GpuTreeHasher:
+    """ledger/tree_hasher.py TreeHasher with the bulk operations on the GPU."""
+
+    def __repr__(self):
+        return 'GpuTreeHasher()'
+
+    def hash_empty(self):
+        return merkle_root([])
+
+    def hash_leaf(self, data):
+        return sha256_batch([data], prefix=0x00)[0]
+
+    def hash_leaves(self, leaves):
+        return sha256_batch(leaves, prefix=0x00)
+
+    def hash_children(self, left, right):
+        return sha256_batch([bytes(left) + bytes(right)], prefix=0x01)[0]
+
+    def hash_full_tree(self, leaves):
+        return merkle_root(leaves)

@@ -26,6 +26,9 @@ Fixtures
                         libsodium crypto_sign_open (framing included)
   tally.npz             25-node COMMIT batches: sender, verdict -> quorum bits via
                         the reference Commits/Quorums (plenum/server/models.py:91-114)
+  merkle.json           Merkle Tree Hash roots (ledger/tree_hasher.py TreeHasher.hash_full_tree,
+                        checked against CompactMerkleTree.extend) over leaves of every length
+                        around the SHA-256 block boundaries, leaf and child hashes
   ingress.json          one node service pass for the batched-ingestion path (f1):
                         client requests of every shape with the reference
                         Request(**req).key (plenum/common/request.py:82-120) and the
@@ -699,7 +702,29 @@ def gen_ingress(n=48):
     return {'registry': registry, 'write_types': ['buy'], 'cases': cases, 'propagates': props, 'batches': batches}
 
 
-GENERATORS = ['kat', 'plenum_requests', 'raw_vectors', 'adversarial', 'tally', 'ingress']
+def gen_merkle():
+    """Merkle Tree Hash roots from the reference ledger/tree_hasher.py TreeHasher
+    (and CompactMerkleTree for the incremental form) over deterministic leaves of
+    every length around the SHA-256 block boundaries."""
+    from ledger.compact_merkle_tree import CompactMerkleTree
+    from ledger.tree_hasher import TreeHasher
+    th = TreeHasher()
+    lens = [0, 1, 2, 31, 32, 54, 55, 56, 62, 63, 64, 65, 118, 119, 120, 127, 128, 129, 255, 256, 1000, 4097]
+    leaves = [det_bytes(b'plenum-gpu/merkle', i, lens[i % len(lens)]) for i in range(1030)]
+    trees = []
+    for size in list(range(0, 70)) + [127, 128, 129, 1000, 1030]:
+        cmt = CompactMerkleTree(hasher=th)
+        cmt.extend(leaves[:size])
+        root = th.hash_full_tree(leaves[:size])
+        assert cmt.root_hash == root
+        trees.append({'size': size, 'root': root.hex()})
+    return {'leaves': [lf.hex() for lf in leaves], 'trees': trees,
+            'leaf_hashes': [th.hash_leaf(lf).hex() for lf in leaves[:70]],
+            'children': [th.hash_children(leaves[i][:32].ljust(32, b'x'), leaves[i + 1][:32].ljust(32, b'y')).hex()
+                         for i in range(0, 20, 2)]}
+
+
+GENERATORS = ['kat', 'plenum_requests', 'raw_vectors', 'adversarial', 'tally', 'ingress', 'merkle']
 
 
 def main(which=None):
@@ -717,6 +742,9 @@ def main(which=None):
         np.savez_compressed(os.path.join(OUT, 'adversarial.npz'), **gen_adversarial())
     if 'tally' in which:
         np.savez_compressed(os.path.join(OUT, 'tally.npz'), **gen_tally())
+    if 'merkle' in which:
+        with open(os.path.join(OUT, 'merkle.json'), 'w') as fh:
+            json.dump(gen_merkle(), fh, indent=0)
     if 'ingress' in which:
         with open(os.path.join(OUT, 'ingress.json'), 'w') as fh:
             json.dump(gen_ingress(), fh, indent=0)

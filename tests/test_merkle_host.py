@@ -1,0 +1,49 @@
+"""Row f3 on CPU: the kernels' SHA-256 block loader and Merkle node (host
+instrumentation build of pv_sha256.h) against hashlib, and the level-wise tree
+shape the GPU uses against the reference TreeHasher / CompactMerkleTree roots."""
+import ctypes
+import hashlib
+import os
+
+import numpy as np
+
+import _merkle as mk
+import _oracle as orc
+from test_hostcheck import _load
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def test_sha256_block_loader_vs_hashlib():
+    hc = _load()
+    rng = np.random.default_rng(5)
+    lens = list(range(0, 140)) + [183, 184, 191, 192, 255, 256, 1000, 4097]
+    msgs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    blob = orc.padded(np.frombuffer(b''.join(msgs), np.uint8))
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    for prefix in (-1, 0, 1, 0xab):
+        out = np.zeros((len(msgs), 32), np.uint8)
+        hc.hc_sha256(_p(blob), _p(off), ctypes.c_uint64(len(msgs)), ctypes.c_int(prefix), _p(out))
+        pre = b'' if prefix < 0 else bytes([prefix])
+        for i, m in enumerate(msgs):
+            assert out[i].tobytes() == hashlib.sha256(pre + m).digest(), (prefix, len(m))
+
+
+def test_sha256_node_vs_hashlib():
+    hc = _load()
+    for _ in range(50):
+        lr = np.frombuffer(os.urandom(64), np.uint8).copy()
+        out = np.zeros(32, np.uint8)
+        hc.hc_sha256_node(_p(lr), _p(out))
+        assert out.tobytes() == hashlib.sha256(b'\x01' + lr.tobytes()).digest()
+
+
+def test_levelwise_shape_matches_reference_roots():
+    fx = mk.fixture()
+    for t in fx['trees']:
+        assert mk.mth_levelwise(fx['leaves'][:t['size']]).hex() == t['root'], t['size']
+    for i, h in enumerate(fx['leaf_hashes']):
+        assert mk.leaf(fx['leaves'][i]).hex() == h

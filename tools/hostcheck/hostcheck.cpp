@@ -53,6 +53,7 @@ static void hc_check_sq(const uint32_t* f) {
 #define PV_CHECK_SQ(f) hc_check_sq((f).v)
 
 #include "../../indy-plenum_amd/csrc/pv_verify_core.h"
+#include "../../indy-plenum_amd/csrc/pv_sha256.h"
 
 using namespace pv;
 
@@ -106,6 +107,20 @@ void hc_verify_keyed(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const 
   free(ktab);
   free(h);
   free(pre);
+}
+
+// SHA-256(prefix || M_i) with the kernels' block loader; prefix < 0 = none
+void hc_sha256(const uint8_t* blob, const uint64_t* off, uint64_t n, int prefix, uint8_t* out) {
+  for (uint64_t i = 0; i < n; ++i)
+    sha256_msg(reinterpret_cast<uint32_t*>(out + 32 * i), blob + off[i], off[i + 1] - off[i], prefix < 0 ? 0 : 1,
+               prefix < 0 ? 0 : (uint32_t)prefix);
+}
+
+// Merkle node SHA-256(0x01 || l || r) with the kernels' fixed-size path
+void hc_sha256_node(const uint8_t* lr64, uint8_t* out) {
+  uint32_t lr[16];
+  memcpy(lr, lr64, 64);
+  sha256_node(reinterpret_cast<uint32_t*>(out), lr);
 }
 
 void hc_sign_batch(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* pk,

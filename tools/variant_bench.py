@@ -32,6 +32,7 @@ def main():
     ap.add_argument('--mlen-max', type=int, default=None)
     ap.add_argument('--key-mod', type=int, default=0)
     ap.add_argument('--cfg', type=int, default=2)
+    ap.add_argument('--no-check', action='store_true', help='timing experiments whose verdicts are knowingly wrong')
     a = ap.parse_args()
     b = SyntheticBatch(0, a.n, a.mlen, cfg=a.cfg, mode=a.mode, mlen_max=a.mlen_max, key_mod=a.key_mod)
     torch.cuda.synchronize()
@@ -56,7 +57,7 @@ def main():
                                            _p(b.bitmap), 0, stream, 2, ctypes.byref(h), ctypes.byref(c))
             assert rc == 0, lib.pv_last_error()
             v = b.verdict.cpu().numpy().astype(bool)
-            assert (v == ~tamper).all(), name
+            assert a.no_check or (v == ~tamper).all(), name
             res[name].append((h.value, c.value))
     out = {}
     for name, vals in res.items():
