@@ -94,3 +94,40 @@ def tally_batches(verdict, sender, batch_off, n_nodes, quorum):
     """
     return _native.tally_arrays(np.asarray(verdict, np.uint8), np.asarray(sender, np.uint32),
                                 np.asarray(batch_off, np.uint64), int(n_nodes), int(quorum))
+
+
+def propagate_quorums(req_keys, senders, verdict, n_nodes, node_index=None):
+    """PROPAGATE f+1 quorum per request (row f4): ReqState.req_with_acceptable_quorum
+    (plenum/server/propagator.py:36-44) over many requests at once with the same
+    GPU tally as COMMITs — one vote per distinct sender whose PROPAGATE carried a
+    valid request signature, reached iff votes >= Quorums(n).propagate (f + 1).
+
+    req_keys (m,) request key of each PROPAGATE, senders (m,) node names (or
+    indices), verdict (m,) bool.  Returns {key: (votes, reached)} in first-seen order.
+    """
+    from .quorums import Quorums
+    order, groups = [], {}
+    for k, key in enumerate(req_keys):
+        if key not in groups:
+            groups[key] = []
+            order.append(key)
+        groups[key].append(k)
+    names = dict(node_index or {})
+    idx = []
+    for s in senders:
+        if isinstance(s, (int, np.integer)):
+            idx.append(int(s))
+        else:
+            if s not in names:
+                names[s] = len(names)
+            idx.append(names[s])
+    flat, off = [], [0]
+    for key in order:
+        flat.extend(groups[key])
+        off.append(len(flat))
+    flat = np.asarray(flat, np.int64)
+    sender = np.asarray(idx, np.uint32)[flat] if len(flat) else np.zeros(0, np.uint32)
+    ver = np.asarray(verdict, bool)[flat] if len(flat) else np.zeros(0, bool)
+    votes, reached = tally_batches(ver, sender, np.asarray(off, np.uint64), max(n_nodes, len(names)),
+                                   Quorums(n_nodes).propagate.value)
+    return {key: (int(votes[j]), bool(reached[j])) for j, key in enumerate(order)}

@@ -43,3 +43,28 @@ def test_tally_random_vs_sets(n_nodes):
                 commits.addVote(c, 'Node%d' % sender[k])
         assert votes[b] == commits._votes_count(c)
         assert reached[b] == commits.hasQuorum(c, q)
+
+
+def test_propagate_f_plus_1_quorums():
+    """Row f4: PROPAGATE f+1 quorums per request through the GPU tally equal the
+    reference ReqState.req_with_acceptable_quorum voter-set semantics."""
+    from plenum_gpu.models import propagate_quorums
+    from plenum_gpu.quorums import Quorums
+    rng = np.random.default_rng(4)
+    n_nodes = 25
+    q = Quorums(n_nodes).propagate
+    keys, senders, verdict = [], [], []
+    for r in range(2000):
+        for _ in range(int(rng.integers(0, 14))):
+            keys.append('req%d' % r)
+            senders.append('Node%d' % int(rng.integers(1, n_nodes + 1)))   # duplicates happen
+            verdict.append(bool(rng.random() < 0.9))
+    got = propagate_quorums(keys, senders, verdict, n_nodes)
+    want = {}
+    for k, s, v in zip(keys, senders, verdict):
+        want.setdefault(k, set())
+        if v:
+            want[k].add(s)
+    assert set(got) == set(want)
+    for k, voters in want.items():
+        assert got[k] == (len(voters), q.is_reached(len(voters))), k

@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU session: full -m gpu suite, every bench config, a rocprofv3 kernel
+# trace of the headline bench and the PMC passes.  Run on the GPU box:
+#   bash tools/gpu_round.sh gpurun_out/round
+# Each GPU step has its own time limit; the script stops at the first failure.
+set -u
+out=${1:-gpurun_out/round}
+mkdir -p "$out"
+step() { echo "[gpu_round] $(date +%T) $1" ; }
+step tests && timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > "$out/gpu_tests.log" 2>&1 && \
+step c2 && timeout -k 10 240 python bench.py > "$out/bench_c2.json" 2> "$out/bench_c2.err" && \
+step c1 && timeout -k 10 240 python bench.py --config c1 > "$out/bench_c1.json" 2> "$out/bench_c1.err" && \
+step c3 && timeout -k 10 240 python bench.py --config c3 > "$out/bench_c3.json" 2> "$out/bench_c3.err" && \
+step c4 && timeout -k 10 300 python bench.py --config c4 --steps 3 --warmup 1 > "$out/bench_c4.json" 2> "$out/bench_c4.err" && \
+step f3 && timeout -k 10 240 python bench.py --config f3 > "$out/bench_f3.json" 2> "$out/bench_f3.err" && \
+step rocprof && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 bench.py --no-cpu-baseline \
+    > "$out/prof.log" 2>&1 && \
+step pmc && bash tools/pmc_passes.sh "$out/pmc" && step done

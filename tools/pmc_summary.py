@@ -22,6 +22,8 @@ def load(d, tag):
         with open(fn) as fh:
             for r in csv.DictReader(fh):
                 k = r['Kernel_Name'].split('(')[0]
+                if k.startswith('void '):
+                    k = k[5:]
                 per[k][r['Counter_Name']].append(float(r['Counter_Value']))
     return per
 
@@ -47,7 +49,7 @@ def main(d):
         if 'GRBM_GUI_ACTIVE' in c:
             e['gpu_cycles_per_xcd'] = c['GRBM_GUI_ACTIVE'] / 8
         out['kernels'][k] = e
-    curve = out['kernels'].get('pv::k_curve', {})
+    curve = next((v for k, v in out['kernels'].items() if k.startswith('pv::k_curve') and 'true' not in k), {})
     out['hbm_bytes_per_launch'] = curve.get('hbm_bytes_per_launch')
     print(json.dumps(out, indent=1))
 
