@@ -312,7 +312,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', choices=sorted(CONFIGS) + ['f3'], default='c2',
                     help='workload (default c2, the headline; f3 = ledger Merkle hashing)')
-    ap.add_argument('--n', type=int, default=None, help='signatures per GPU (default: the config\'s)')
+    ap.add_argument('--n', '--count', dest='n', type=int, default=None,
+                    help='signatures per GPU (default: the config\'s); spell it --count under torch.distributed.run')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-key-cache', action='store_true',
                     help='c3/c4: re-decompress every key per signature instead of preparing each distinct key once')
@@ -325,10 +326,30 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # production: one rank per GPU over RCCL ("nccl").  Rehearsal of the N > 1
+    # path on a one-GPU box: PV_BENCH_BACKEND=gloo PV_BENCH_SHARE_GPU=1 puts every
+    # rank on GPU 0 and runs the same collectives through host copies.
+    backend = os.environ.get('PV_BENCH_BACKEND', 'nccl')
+    if os.environ.get('PV_BENCH_SHARE_GPU') == '1':
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    def coll_dev(t):
+        return t if backend == 'nccl' else t.cpu()
+
+    def all_gather(out, inp):
+        if backend == 'nccl':
+            dist.all_gather_into_tensor(out, inp)
+        else:
+            o = out.cpu()
+            dist.all_gather_into_tensor(o, inp.cpu())
+            out.copy_(o)
 
     cfg = CONFIGS[args.config]
     n = args.n or cfg['n']
@@ -355,9 +376,9 @@ def main():
             tally_device(batch.verdict, batch.sender, tally['boff'], n_nodes, tally['q'], tally['votes'],
                          tally['reached'])
         if world > 1:
-            dist.all_gather_into_tensor(gathered, batch.bitmap)
+            all_gather(gathered, batch.bitmap)
             if tally is not None:   # C3: batch-sharded tallies, gather the quorum bits
-                dist.all_gather_into_tensor(tally['gathered'], tally['reached'])
+                all_gather(tally['gathered'], tally['reached'])
 
     for _ in range(args.warmup):
         step()
@@ -374,7 +395,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = coll_dev(torch.tensor([elapsed], dtype=torch.float64, device=dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -392,11 +413,20 @@ def main():
             _, all_reached = synth.c3_expected(0, world * tally['nb'], n_nodes, tally['q'])
             mism += int((tally['gathered'].cpu().numpy().astype(bool) != all_reached).sum())
     if world > 1:
-        allbits = np.unpackbits(gathered.cpu().numpy().view(np.uint8), bitorder='little')
+        # own slice of the gathered bitmaps == own verdicts, and every rank holds
+        # the same gathered bytes (checksums equal under MIN and MAX)
+        g = gathered.cpu().numpy()
+        allbits = np.unpackbits(g.view(np.uint8), bitorder='little')
         per = batch.bitmap.numel() * 64
         mine = allbits[rank * per: rank * per + n].astype(bool)
         mism += int((mine != verdict).sum())
-        m = torch.tensor([mism], dtype=torch.int64, device=dev)
+        import hashlib
+        ck = int.from_bytes(hashlib.sha256(g.tobytes()).digest()[:7], 'little')
+        cks = [coll_dev(torch.tensor([ck], dtype=torch.int64, device=dev)) for _ in range(2)]
+        dist.all_reduce(cks[0], op=dist.ReduceOp.MIN)
+        dist.all_reduce(cks[1], op=dist.ReduceOp.MAX)
+        mism += int(cks[0].item() != cks[1].item())
+        m = coll_dev(torch.tensor([mism], dtype=torch.int64, device=dev))
         dist.all_reduce(m)
         mism = int(m.item())
 
@@ -419,7 +449,8 @@ def main():
                    'key_pool': cfg['key_mod'] or ('node keys' if cfg['mode'] == synth.COMMIT else 'distinct'),
                    'key_cache': 'prepared once per step per distinct key (inside the timed step)' if key_cache
                    else 'off', 'tampered': int(tamper.sum()),
-                   'parallelism': 'dp{} (disjoint index shards) + RCCL all-gather of verdict bitmaps'.format(world)
+                   'parallelism': 'dp{} (disjoint index shards) + {} all-gather of verdict bitmaps'.format(
+                       world, 'RCCL' if backend == 'nccl' else backend + ' (rehearsal, ranks share GPU 0)')
                    if world > 1 else 'single GPU'},
         'verdict_mismatches': mism,
         'kernel_ms': {'hash': round(ms_hash, 4), 'curve': round(ms_curve, 4)},
