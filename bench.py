@@ -56,12 +56,20 @@ CONFIGS = {
 # Algorithmic work of the curve kernel per verify, counted by the host
 # instrumentation build of the same code (tests/test_hostcheck.py pins these):
 # field multiplies x 100 + squarings x 55 v_mad_u64_u32 (radix 2^25.5 schoolbook).
-# (the final Z^-1 is shared by CURVE_K = 4 signatures per lane: 3 of every 4
-# 254-squaring inversions are replaced by 3 multiplies; the decompression
-# multiplies by sqrt(-1) for about half of all keys, hence the .5)
-W_MUL_PER_VERIFY = 1581.5
-W_SQ_PER_VERIFY = 1326.5
+# Generic batches (PV_CURVE_MODE=half, the default): half-size scalars, 128
+# doublings; decompression of -A and -R (each multiplies by sqrt(-1) for about
+# half of all points: the mean is a whole number of multiplies), two 9-entry
+# tables, 33 windows, identity test instead of an inversion.  Deferred records
+# (~0.2 %) take the full-length verdict (W_*_FULL: 253 doublings + inversion).
+W_MUL_PER_VERIFY = 1299.0
+W_SQ_PER_VERIFY = 1022.0
 W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
+W_MUL_FULL, W_SQ_FULL = 1587.5, 1517.0
+W_MAD_FULL = int(W_MUL_FULL * 100 + W_SQ_FULL * 55)
+# PV_CURVE_MODE=grouped: full-length scalars, CURVE_K = 4 signatures per lane
+# sharing one inversion (3 of every 4 254-squaring inversions become 3 multiplies)
+W_MUL_GROUPED, W_SQ_GROUPED = 1581.5, 1326.5
+W_MAD_GROUPED = int(W_MUL_GROUPED * 100 + W_SQ_GROUPED * 55)
 # keyed batches (prepared keys, 4-way comb of -A): 60 doublings instead of 256,
 # no decompression; decompression, the comb tables (3 x 61 doublings, 32 affine
 # multiples, one shared inversion) run once per distinct key in k_keys
@@ -432,8 +440,20 @@ def main():
 
     # kernel-level timing (HIP events on the launch stream) for the roofline
     ms_hash, ms_curve = batch.time_kernels(3)
-    w_mad = W_MAD_KEYED if key_cache else W_MAD_PER_VERIFY
-    achieved = w_mad * n / (ms_curve * 1e-3)
+    curve_mode, deferred = nat.curve_stats(local)
+    if key_cache:
+        kernel, work = 'k_curve<keyed>', W_MAD_KEYED * n
+        wpv = {'fe_mul': W_MUL_KEYED, 'fe_sq': W_SQ_KEYED, 'mad': W_MAD_KEYED,
+               'per_distinct_key': {'fe_mul': W_MUL_KEYPREP, 'fe_sq': W_SQ_KEYPREP}}
+    elif curve_mode == 'grouped':
+        kernel, work = 'k_curve', W_MAD_GROUPED * n
+        wpv = {'fe_mul': W_MUL_GROUPED, 'fe_sq': W_SQ_GROUPED, 'mad': W_MAD_GROUPED}
+    else:
+        kernel, work = 'k_curve_half', W_MAD_PER_VERIFY * (n - deferred) + W_MAD_FULL * deferred
+        wpv = {'fe_mul': W_MUL_PER_VERIFY, 'fe_sq': W_SQ_PER_VERIFY, 'mad': W_MAD_PER_VERIFY,
+               'deferred_full_length': {'count': deferred, 'fe_mul': W_MUL_FULL, 'fe_sq': W_SQ_FULL,
+                                        'mad': W_MAD_FULL}}
+    achieved = work / (ms_curve * 1e-3)
     peak = _mad_peak()
 
     total = world * n * args.steps
@@ -454,15 +474,12 @@ def main():
                    if world > 1 else 'single GPU'},
         'verdict_mismatches': mism,
         'kernel_ms': {'hash': round(ms_hash, 4), 'curve': round(ms_curve, 4)},
-        'roofline': {'bound': 'valu', 'kernel': 'k_curve',
+        'roofline': {'bound': 'valu', 'kernel': kernel,
                      'achieved': round(achieved / 1e12, 3), 'peak': round(peak / 1e12, 3),
                      'unit': 'Tmad/s (v_mad_u64_u32 lane-ops)', 'frac': round(achieved / peak, 4),
                      'traffic': _traffic_per_launch() if (args.config, n) == ('c2', CONFIGS['c2']['n']) else None,
-                     'work_per_verify': ({'fe_mul': W_MUL_KEYED, 'fe_sq': W_SQ_KEYED, 'mad': W_MAD_KEYED,
-                                          'per_distinct_key': {'fe_mul': W_MUL_KEYPREP, 'fe_sq': W_SQ_KEYPREP}}
-                                         if key_cache else
-                                         {'fe_mul': W_MUL_PER_VERIFY, 'fe_sq': W_SQ_PER_VERIFY,
-                                          'mad': W_MAD_PER_VERIFY})},
+                     'work_per_verify': wpv},
+        'curve_mode': curve_mode if not key_cache else 'keyed',
         'cpu_baseline': None,
     }
     if tally is not None:

@@ -187,10 +187,32 @@ int pv_synth_device(uint32_t cfg, uint64_t first, uint64_t n, uint32_t key_mod, 
 
 /* Time the verify kernels alone over `iters` launches on device-resident
  * inputs using HIP events on the launch stream; returns per-kernel average
- * milliseconds (hash, curve). */
+ * milliseconds (hash, curve).  "hash" = k_hash plus, on the half-size path, the
+ * scalar stage k_lattice; "curve" = the single curve kernel launch. */
 int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
                           uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device, void *stream, int iters,
                           float *ms_hash, float *ms_curve);
+
+/* Curve-stage schedule of generic (non-keyed) batches on `device`, chosen by
+ * the environment variable PV_CURVE_MODE at pv_init:
+ *   PV_CURVE_HALF     (default, "half") half-size scalars: Euclid on (8L, h)
+ *                     gives c == d h (mod 8L) with |c|, d < 2^131, d odd, and the
+ *                     verdict is  s'B + c(-A) + d(-R) == O  (s' = dS mod L): the
+ *                     same accept/reject as libsodium's encode(SB - hA) == R for
+ *                     every input (derivation in indy-plenum_amd/csrc/pv_lattice.h);
+ *                     the ~0.2 % of signatures whose h has no such (c, d) get the
+ *                     full-length verdict in the same launch;
+ *   PV_CURVE_FULL     ("full") every signature through the full-length verdict;
+ *   PV_CURVE_GROUPED  ("grouped") the full-length kernel with 4 signatures per
+ *                     lane sharing one inversion.
+ * pv_set_curve_mode switches every initialised device (A/B timing, tests).
+ * deferred (may be NULL) = signatures of the last generic batch on this device
+ * that took the full-length verdict (0 if none ran). */
+#define PV_CURVE_HALF 0u
+#define PV_CURVE_FULL 1u
+#define PV_CURVE_GROUPED 2u
+int pv_set_curve_mode(uint32_t mode);
+int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 
 /* pv_time_verify_device for keyed batches. */
 int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk, const uint8_t *sig,

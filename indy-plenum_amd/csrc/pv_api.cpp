@@ -9,6 +9,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -63,6 +64,13 @@ struct DevBuf {
   }
 };
 
+// PV_CURVE_MODE (read at pv_init): "half" (default) = half-size scalars with
+// full-length tasks for deferred records; "full" = every record deferred
+// (full-length verdicts through the same kernel: A/B timing and tests);
+// "grouped" = the previous generic kernel (k_curve, 4 signatures per lane
+// sharing one inversion).  Verdicts are identical in every mode.
+enum class CurveMode { Half, Full, Grouped };
+
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
@@ -85,6 +93,12 @@ struct Device {
   DevBuf<uint32_t> mk0, mk1;    // Merkle level ping-pong / leaf digests
   int sha256_blocks = 0;
   int curve_blocks_keyed = 0;
+  // generic (unkeyed) batches: half-size scalar path (k_lattice + k_curve_half)
+  DevBuf<uint32_t> hrec, dlist;        // lattice records, deferred indices
+  DevBuf<unsigned long long> qc;       // [0] deferred count, [1] curve task queue
+  int curve_half_blocks = 0;
+  CurveMode mode = CurveMode::Half;
+  bool half_ran = false;               // qc[0] holds the last generic batch's deferred count
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -121,7 +135,21 @@ int init_device(Device& d) {
   if (per_cu < 1) per_cu = 1;
   if (per_cu > 4) per_cu = 4;
   d.curve_blocks = d.cu_count * per_cu;
-  HIP_OK(d.scratch.ensure((size_t)d.curve_blocks * pv::CURVE_BLOCK * pv::ATAB_WORDS));
+  int halfper = 0;
+  HIP_OK(pv::curve_half_occupancy(&halfper));
+  if (halfper < 1) halfper = 1;
+  if (halfper > 4) halfper = 4;
+  d.curve_half_blocks = d.cu_count * halfper;
+  {
+    const size_t a = (size_t)d.curve_blocks * pv::ATAB_WORDS, b = (size_t)d.curve_half_blocks * pv::HALF_SCRATCH_WORDS;
+    HIP_OK(d.scratch.ensure((a > b ? a : b) * pv::CURVE_BLOCK));
+  }
+  HIP_OK(d.qc.ensure(2));
+  if (const char* m = getenv("PV_CURVE_MODE")) {
+    if (!strcmp(m, "full")) d.mode = CurveMode::Full;
+    else if (!strcmp(m, "grouped")) d.mode = CurveMode::Grouped;
+    else if (strcmp(m, "half") != 0) return fail(PV_EINVAL, "PV_CURVE_MODE must be half, full or grouped (got %s)", m);
+  }
   int kper = 0;
   HIP_OK(pv::curve_occupancy(&kper, true));
   if (kper < 1) kper = 1;
@@ -149,6 +177,7 @@ void release_device(Device& d) {
   d.off.release(); d.bitmap.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
   d.ktab.release(); d.kidx.release(); d.kscr.release(); d.mk0.release(); d.mk1.release();
+  d.hrec.release(); d.dlist.release(); d.qc.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -168,11 +197,28 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
     HIP_OK(d.bitmap.ensure((n + 63) / 64));
     bm = d.bitmap.p;
   }
+  const bool half = !ktab && d.mode != CurveMode::Grouped;
+  if (half) {
+    if (n > 0xffffffffull) return fail(PV_EINVAL, "at most 2^32-1 signatures per device call");
+    HIP_OK(d.hrec.ensure(n * pv::HSREC_WORDS));
+    HIP_OK(d.dlist.ensure(n));
+  }
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
   HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.counter.p, d.h.p, d.pre.p, d.hash_blocks, s, kidx));
+  // the "hash" interval also holds the scalar stage of the half-size path
+  if (half)
+    HIP_OK(pv::launch_lattice(sig, d.h.p, d.pre.p, n, d.hrec.p, d.dlist.p, d.qc.p, d.qc.p + 1, bm,
+                              d.mode == CurveMode::Full, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
-  HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict, bm,
-                          n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx));
+  if (half) {
+    HIP_OK(pv::launch_curve_half(pk, sig, d.h.p, d.hrec.p, d.btab.p, d.scratch.p,
+                                 d.scratch.cap / pv::HALF_SCRATCH_WORDS, verdict, bm, n, d.dlist.p, d.qc.p, d.qc.p + 1,
+                                 d.curve_half_blocks, s));
+    d.half_ran = true;
+  } else {
+    HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict,
+                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx));
+  }
   if (timed) {
     HIP_OK(hipEventRecord(d.ev[2], s));
     HIP_OK(hipEventSynchronize(d.ev[2]));
@@ -404,6 +450,35 @@ int pv_time_verify_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
   }
   if (ms_hash) *ms_hash = a / iters;
   if (ms_curve) *ms_curve = b / iters;
+  return PV_OK;
+}
+
+int pv_set_curve_mode(uint32_t mode) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (mode > PV_CURVE_GROUPED) return fail(PV_EINVAL, "unknown curve mode %u", mode);
+  for (auto& d : g_devs) {
+    d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
+    d.half_ran = false;
+  }
+  return PV_OK;
+}
+
+int pv_curve_stats(int device, uint32_t* mode, uint64_t* deferred) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (mode) *mode = d->mode == CurveMode::Half ? PV_CURVE_HALF : d->mode == CurveMode::Full ? PV_CURVE_FULL
+                                                                                             : PV_CURVE_GROUPED;
+  if (deferred) {
+    *deferred = 0;
+    if (d->half_ran) {
+      HIP_OK(hipSetDevice(device));
+      HIP_OK(hipStreamSynchronize(d->stream));
+      HIP_OK(hipMemcpy(deferred, d->qc.p, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
+  }
   return PV_OK;
 }
 

@@ -45,6 +45,24 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab = nullptr,
                         const uint32_t* kidx = nullptr);
 
+// Half-size scalar path (generic batches, pv_lattice.h):
+//   launch_lattice   h mod L -> (c, d, s') records (HSREC_WORDS words per
+//                    signature), deferred indices -> dlist / *dcount; also
+//                    zeroes *tasks and the bitmap (ceil(n/64) words) the curve
+//                    kernel ORs into.  n < 2^32.
+//   launch_curve_half  verdicts + bitmap; per-lane scratch HALF_SCRATCH_WORDS
+//                    (tables of +-A and -R).
+constexpr int HSREC_WORDS = 20;
+constexpr int HALF_SCRATCH_WORDS = 2 * 9 * 40;
+hipError_t curve_half_occupancy(int* blocks_per_cu);
+hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t* pre, uint64_t n, uint32_t* rec,
+                          uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks, uint64_t* bitmap,
+                          bool force_full, hipStream_t s);
+hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, const uint32_t* rec,
+                             const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
+                             uint64_t* bitmap, uint64_t n, const uint32_t* dlist, const unsigned long long* dcount,
+                             unsigned long long* tasks, int blocks, hipStream_t s);
+
 // prepared keys: KEYTAB_WORDS words per key (4 comb tables of affine multiples
 // k * 2^(64 q) * (-A) + status); KEYTAB_SCRATCH words of scratch per key
 constexpr int KEYTAB_WORDS = 4 * 9 * 32 + 8;

@@ -26,7 +26,8 @@ namespace pv {
 #endif
 
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
-                  KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && COMB_Q == BTAB_QUARTERS,
+                  KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && COMB_Q == BTAB_QUARTERS &&
+                  HREC_WORDS == HSREC_WORDS && HALF_LANE_WORDS == HALF_SCRATCH_WORDS,
               "table layout");
 
 // ------------------------------------------------------------- hash kernel
@@ -187,6 +188,115 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
   else
     hipLaunchKernelGGL(k_curve<false>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
                        verdict, bitmap, n, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------ half-size scalar path
+// k_lattice: one lane per signature.  h = digest mod L, Euclid on (8L, h) ->
+// (c, d), s' = d S mod L, written as the record the curve kernel reads;
+// deferred indices (~0.2 %) are appended to `dlist` (wave-aggregated atomic).
+__global__ __launch_bounds__(256) void k_lattice(const uint8_t* __restrict__ sig, const uint32_t* __restrict__ dig,
+                                                  const uint8_t* __restrict__ pre, uint64_t n,
+                                                  uint32_t* __restrict__ rec, uint32_t* __restrict__ dlist,
+                                                  unsigned long long* __restrict__ dcount, int force_full) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t st = HS_NONE;
+  if (i < n) st = lattice_one(rec + HREC_WORDS * i, pre[i] != 0, dig + 16 * i, sig + 64 * i, force_full != 0);
+  const bool defer = st == HS_DEFER;
+  const uint64_t m = __ballot(defer);
+  if (m) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(dcount, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (defer) dlist[base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+  }
+}
+
+// k_curve_half: persistent grid over a wave-granular work queue.  Tasks
+// [0, F) are full-length verdicts of 64 deferred records each (taken first:
+// they are the longest), tasks [F, F + ceil(n/64)) are 64 consecutive
+// signatures on the half-size path (lanes of deferred or pre-rejected
+// records idle).  Every task ORs its accepted bits into the bitmap (zeroed
+// before the launch), so the two kinds never overwrite each other's words.
+// LDS: tables of B and 2^128 B (2 x 16.5 KB).
+__global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint32_t* __restrict__ dig,
+    const uint32_t* __restrict__ rec, const uint32_t* __restrict__ btab_g, uint32_t* __restrict__ scratch,
+    uint8_t* __restrict__ verdict, unsigned long long* __restrict__ bitmap, uint64_t n,
+    const uint32_t* __restrict__ dlist, const unsigned long long* __restrict__ dcount,
+    unsigned long long* __restrict__ tasks) {
+  constexpr int TW = BTAB_ENTRIES * BTAB_WORDS;
+  __shared__ uint32_t btab[2 * TW];
+  for (int j = threadIdx.x; j < TW; j += CURVE_BLOCK) {
+    btab[j] = btab_g[j];                 // q = 0: B
+    btab[TW + j] = btab_g[2 * TW + j];   // q = 2: 2^128 B
+  }
+  __syncthreads();
+  const int lane = (int)(threadIdx.x & 63u);
+  uint32_t* scr = scratch + ((uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x) * HALF_LANE_WORDS;
+  const uint64_t nd = *dcount;
+  const uint64_t full_tasks = (nd + 63) / 64;
+  const uint64_t all_tasks = full_tasks + (n + 63) / 64;
+  for (;;) {
+    unsigned long long t = 0;
+    if (lane == 0) t = atomicAdd(tasks, 1ull);
+    t = __shfl(t, 0, 64);
+    if (t >= all_tasks) break;
+    if (t < full_tasks) {
+      const uint64_t j = t * 64 + lane;
+      if (j < nd) {
+        const uint64_t i = dlist[j];
+        const bool ok = verify_full_one(pk + 32 * i, sig + 64 * i, dig + 16 * i, scr, btab);
+        verdict[i] = ok ? 1 : 0;
+        if (ok) atomicOr(&bitmap[i >> 6], 1ull << (i & 63));
+      }
+    } else {
+      const uint64_t i = (t - full_tasks) * 64 + lane;
+      uint32_t st = HS_NONE;
+      if (i < n) st = rec[HREC_WORDS * i + HREC_FLAGS] & 0xffu;
+      bool ok = false;
+      if (st == HS_HALF) ok = curve_half(pk + 32 * i, sig + 64 * i, rec + HREC_WORDS * i, scr, btab, btab + TW);
+      const uint64_t ball = __ballot(ok);
+      if (i < n && st != HS_DEFER) verdict[i] = ok ? 1 : 0;
+      if (lane == 0 && ball) atomicOr(&bitmap[t - full_tasks], (unsigned long long)ball);
+    }
+  }
+}
+
+hipError_t curve_half_occupancy(int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_curve_half),
+                                                      CURVE_BLOCK, 0);
+}
+
+hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t* pre, uint64_t n, uint32_t* rec,
+                          uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks, uint64_t* bitmap,
+                          bool force_full, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n > 0xffffffffull) return hipErrorInvalidValue;  // deferred indices are 32-bit
+  // counters and the bitmap the curve kernel ORs into are reset here, so that
+  // the curve launch is a single kernel (its HIP-event time == rocprof's)
+  hipError_t e = hipMemsetAsync(dcount, 0, sizeof(unsigned long long), s);
+  if (e == hipSuccess) e = hipMemsetAsync(tasks, 0, sizeof(unsigned long long), s);
+  if (e == hipSuccess) e = hipMemsetAsync(bitmap, 0, ((n + 63) / 64) * sizeof(uint64_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lattice, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sig, dig, pre, n, rec, dlist,
+                     dcount, force_full ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, const uint32_t* rec,
+                             const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
+                             uint64_t* bitmap, uint64_t n, const uint32_t* dlist, const unsigned long long* dcount,
+                             unsigned long long* tasks, int blocks, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t need = (n + CURVE_BLOCK - 1) / CURVE_BLOCK;
+  uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
+  if (b * CURVE_BLOCK > scratch_lanes) b = scratch_lanes / CURVE_BLOCK;
+  if (b == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_curve_half, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, dig, rec, btab, scratch,
+                     verdict, reinterpret_cast<unsigned long long*>(bitmap), n, dlist, dcount, tasks);
   return hipGetLastError();
 }
 

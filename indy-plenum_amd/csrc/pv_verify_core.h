@@ -12,6 +12,7 @@
 #include "pv_scalar.h"
 #include "pv_curve.h"
 #include "pv_sha512.h"
+#include "pv_lattice.h"
 
 namespace pv {
 
@@ -687,6 +688,174 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     accepted |= (diff == 0 ? 1u : 0u) << k;
   }
   return accepted;
+}
+
+// ------------------------------------------------- half-size scalar path
+// Per-signature record written by the lattice stage (k_lattice) and read by
+// the curve stage: |c|, d in their signed-digit offset form (33 nibbles),
+// s' = d S mod L in radix-256 offset form, and a status word
+// (HS_NONE: rejected before the curve, HS_HALF, HS_DEFER) | c_neg << 8.
+constexpr int HREC_WORDS = 20;
+constexpr int HREC_C = 0, HREC_D = 5, HREC_S = 10, HREC_FLAGS = 18;
+constexpr int HALF_LANE_WORDS = 2 * AT_WORDS;   // tables of +-A and -R
+
+// pre = the hash stage's pre-check verdict; dig = SHA-512(R||A||M)
+PV_HD uint32_t lattice_one(uint32_t* rec, bool pre, const uint32_t* dig, const uint8_t* sig, bool force_full) {
+  uint32_t st = HS_NONE;
+  bool c_neg = false;
+  if (pre) {
+    st = HS_DEFER;
+    if (!force_full) {
+      uint32_t h[8], c[HS_WORDS], d[HS_WORDS];
+      {
+        uint32_t x[16];
+        load8(x, reinterpret_cast<const uint8_t*>(dig));
+        load8(x + 8, reinterpret_cast<const uint8_t*>(dig + 8));
+        sc_reduce64(h, x);  // h = SHA-512(R||A||M) mod L (App. C.2 step 5)
+      }
+      st = half_scalars(c, d, c_neg, h);
+      if (st == HS_HALF) {
+        uint32_t S[8], sp[8];
+        load8(S, sig + 32);
+        sc_mul_small(sp, d, S);
+        sc_add_pattern(sp, sp, 0x80808080u);
+        hs_offset(c);
+        hs_offset(d);
+#pragma unroll
+        for (int k = 0; k < HS_WORDS; ++k) {
+          rec[HREC_C + k] = c[k];
+          rec[HREC_D + k] = d[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rec[HREC_S + k] = sp[k];
+      }
+    }
+  }
+  rec[HREC_FLAGS] = st | (c_neg ? 0x100u : 0u);
+  return st;
+}
+
+// Q = s' B + c (+-A) + d (-R) over 33 radix-16 windows (c, d) with the
+// radix-256 digits of s' split over the tables of B (low 16 bytes) and
+// 2^128 B (high 16 bytes), both added on even windows.  Horner from the top:
+// per window 4 doublings, one add from each per-lane table, and on even
+// windows two base-point adds.  Leaves the last sum in p1p1 form.
+PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const uint32_t* rtab, const uint32_t* blo,
+                    const uint32_t* bhi) {
+  uint32_t cp[4], dp[4], sl[4], sh[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    cp[k] = rec[HREC_C + k];
+    dp[k] = rec[HREC_D + k];
+    sl[k] = rec[HREC_S + k];
+    sh[k] = rec[HREC_S + 4 + k];
+  }
+  ge_p3 acc;
+  ge_p2 r2;
+  ge_p3_0(acc);
+  {
+    const int dA = (int)(rec[HREC_C + 4] & 15u) - 8;
+    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
+    ge_p1p1_to_p3(acc, t);
+    const int dR = (int)(rec[HREC_D + 4] & 15u) - 8;
+    ge_add_cached_at(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY, dR < 0);
+    ge_p1p1_to_p2(r2, t);
+  }
+  uint32_t cw = cp[3], dw = dp[3], lw = sl[3], hw = sh[3];
+#pragma unroll 1
+  for (int w = 31; w >= 0; --w) {
+    if ((w & 7) == 7 && w != 31) {
+      // next lower digit word, static indices only (no scratch spill of the arrays)
+#pragma unroll
+      for (int k = 3; k > 0; --k) {
+        cp[k] = cp[k - 1];
+        dp[k] = dp[k - 1];
+        sl[k] = sl[k - 1];
+        sh[k] = sh[k - 1];
+      }
+      cw = cp[3];
+      dw = dp[3];
+      lw = sl[3];
+      hw = sh[3];
+    }
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+      ge_p2_dbl(t, r2);
+      ge_p1p1_to_p2(r2, t);
+    }
+    ge_p2_dbl(t, r2);
+    ge_p1p1_to_p3(acc, t);
+    const int sh4 = 4 * (w & 7);
+    const int dA = (int)((cw >> sh4) & 15u) - 8;
+    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
+    ge_p1p1_to_p3(acc, t);
+    const int dR = (int)((dw >> sh4) & 15u) - 8;
+    ge_add_cached_at(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY, dR < 0);
+    if ((w & 1) == 0) {
+      const int sh8 = 8 * ((w >> 1) & 3);
+      const int dL = (int)((lw >> sh8) & 255u) - 128;
+      const int dH = (int)((hw >> sh8) & 255u) - 128;
+      ge_p1p1_to_p3(acc, t);
+      ge_madd_at(t, acc, blo + (dL < 0 ? -dL : dL) * BT_WORDS, dL < 0);
+      ge_p1p1_to_p3(acc, t);
+      ge_madd_at(t, acc, bhi + (dH < 0 ? -dH : dH) * BT_WORDS, dH < 0);
+    }
+    if (w == 0) break;
+    ge_p1p1_to_p2(r2, t);
+  }
+}
+
+// p1p1 ((X:Z),(Y:T)) is the identity iff x = 0 and y = 1, i.e. X == 0 and Y == T
+PV_HD bool p1p1_is_identity(const ge_p1p1& p) {
+  fe u;
+  fe_sub4(u, p.Y, p.T);
+  fe_carry(u);
+  return fe_iszero(p.X) && fe_iszero(u);
+}
+
+// The half-size verdict for a HS_HALF record (see pv_lattice.h):
+// accept iff -A and -R decode and s' B + c (-A) + d (-R) == O.  R's y must be
+// canonical (a non-canonical R never equals an encoding libsodium computes).
+// scratch = HALF_LANE_WORDS words of this lane; blo/bhi = tables of B, 2^128 B.
+PV_HD bool curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, uint32_t* scratch,
+                      const uint32_t* blo, const uint32_t* bhi) {
+  ge_p3 P;
+  {
+    uint32_t A[8];
+    load8(A, pk);
+    if (!ge_frombytes_negate(P, A)) return false;  // -A (A canonical: hash-stage pre-check)
+  }
+  if (rec[HREC_FLAGS] & 0x100u) {                // c < 0: c (-A) = |c| A
+    fe_neg(P.X, P.X);
+    fe_carry(P.X);
+    fe_neg(P.T, P.T);
+    fe_carry(P.T);
+  }
+  build_atab(scratch, P);
+  {
+    uint32_t R[8];
+    load8(R, sig);
+    if (!y_is_canonical(R) || !ge_frombytes_negate(P, R)) return false;  // -R
+  }
+  build_atab(scratch + AT_WORDS, P);
+  ge_p1p1 t;
+  msm_half(t, rec, scratch, scratch + AT_WORDS, blo, bhi);
+  return p1p1_is_identity(t);
+}
+
+// Full-length verdict of one signature (deferred records): R' = h(-A) + S B,
+// encode, compare.  scratch = AT_WORDS words; btab = table of B.
+PV_HD bool verify_full_one(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, uint32_t* scratch,
+                           const uint32_t* btab) {
+  ge_p2 rp;
+  if (!curve_point(rp, pk, sig, dig, scratch, btab)) return false;
+  uint32_t enc[8], R[8];
+  ge_p2_tobytes(enc, rp);
+  load8(R, sig);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) diff |= enc[w] ^ R[w];
+  return diff == 0;
 }
 
 // ------------------------------------------------------------ batch signer

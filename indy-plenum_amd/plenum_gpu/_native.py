@@ -54,7 +54,24 @@ SIGNATURES = [
     ('pv_time_verify_device', ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int,
       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+    ('pv_curve_stats', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)]),
+    ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
 ]
+
+CURVE_MODES = {0: 'half', 1: 'full', 2: 'grouped'}   # PV_CURVE_HALF / _FULL / _GROUPED
+
+
+def set_curve_mode(name):
+    """Curve-stage schedule of generic batches on every initialised device (pv_set_curve_mode)."""
+    code = {v: k for k, v in CURVE_MODES.items()}[name]
+    _check('pv_set_curve_mode', load().pv_set_curve_mode(code))
+
+
+def curve_stats(device=0):
+    """(mode name, deferred count of the last generic batch) on `device` (pv_curve_stats)."""
+    mode, nd = ctypes.c_uint32(), ctypes.c_uint64()
+    _check('pv_curve_stats', load().pv_curve_stats(device, ctypes.byref(mode), ctypes.byref(nd)))
+    return CURVE_MODES[mode.value], nd.value
 
 
 class PlenumGpuError(RuntimeError):

@@ -65,6 +65,42 @@ def test_c2_full_size_properties(torch_dev):
     assert (want == v1[idx].astype(bool)).all()
 
 
+def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
+    """The half-size path (default), every record through its full-length
+    tasks (PV_CURVE_MODE=full) and the grouped kernel give identical verdicts
+    and bitmaps; the half path's deferred records really ran (C2-shaped batch)."""
+    from plenum_gpu import _native as nat
+    from plenum_gpu.device import SyntheticBatch
+    from plenum_gpu.nacl_wrappers import verify_signed_batch
+    from conftest import split_sm
+    n = 200_000
+    b = SyntheticBatch(0, n, 256, cfg=2, first=777)
+    tamper = b.tamper.cpu().numpy().astype(bool)
+    rows = split_sm(adversarial)
+    r = raw_vectors
+    try:
+        for mode in ('half', 'full', 'grouped'):
+            nat.set_curve_mode(mode)
+            b.bitmap.fill_(-1)     # the half path must clear it itself
+            v = b.verify().cpu().numpy().astype(bool)
+            got_mode, deferred = nat.curve_stats(0)
+            assert got_mode == mode
+            if mode == 'half':
+                assert 0 < deferred < n // 100      # ~0.2 % of random h
+            elif mode == 'full':
+                assert deferred == int((~tamper).sum()) or deferred >= n * 0.9
+            assert (v == ~tamper).all(), mode
+            bits = np.unpackbits(b.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
+            assert (bits == v).all(), mode
+            got = nat.verify_batch_arrays(r['pk'], r['sig'], r['blob'], r['off'])
+            assert (got == r['verdict'].astype(bool)).all(), mode
+            got = verify_signed_batch([(pk, sm) for _, pk, sm, _ in rows])
+            wrong = [rows[k][0] for k in range(len(rows)) if got[k] != rows[k][3]]
+            assert not wrong, (mode, wrong)
+    finally:
+        nat.set_curve_mode('half')
+
+
 def test_kernel_timer(torch_dev):
     from plenum_gpu.device import SyntheticBatch
     b = SyntheticBatch(0, 65536, 256, cfg=2)

@@ -131,25 +131,126 @@ def test_scalar_reduce_and_muladd_vs_bigint(hc):
         assert int.from_bytes(out.raw, 'little') == (a * b + c) % L
 
 
-def test_op_counts_pin_bench_constants(hc):
-    """The curve kernel's algorithmic work per verify (bench.py W_*), counted on
-    the exact kernel schedule: groups of CURVE_K = 4 signatures share the final
-    inversion."""
-    import bench
-    n = 16
-    seeds = np.frombuffer(os.urandom(32 * n), np.uint8).reshape(n, 32)
-    blob = np.frombuffer(os.urandom(256 * n), np.uint8)
+def _signed_batch(n, seed):
+    rng = np.random.default_rng(seed)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    blob = rng.integers(0, 256, 256 * n, dtype=np.uint8)
     off = np.arange(n + 1, dtype=np.uint64) * 256
     pk, sig = orc.sign_batch(seeds, blob, off)
-    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())  # base-point table outside the counted region
+    return pk, sig, blob, off
+
+
+def _run_mode(hc, pk, sig, blob, off, force_full):
+    n = len(pk)
+    v = np.zeros(n, np.uint8)
+    nd = ctypes.c_uint64()
+    b = orc.padded(blob)
+    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())  # base-point tables outside the counted region
     hc.hc_reset_counts()
-    assert hc_verify(hc, pk, sig, blob, off).all()
+    hc.hc_verify_batch_mode(_p(np.ascontiguousarray(pk)), _p(np.ascontiguousarray(sig)), _p(b),
+                            _p(np.ascontiguousarray(off)), ctypes.c_uint64(n), _p(v), int(force_full), ctypes.byref(nd))
     c, bad = counts(hc)
-    assert bad == 0
+    assert bad == 0, 'a field-multiply input exceeded the LOOSE bound'
+    return v.astype(bool), c, nd.value
+
+
+def test_op_counts_pin_bench_constants(hc):
+    """The curve stage's algorithmic work per verify (bench.py W_*), counted on
+    the exact kernel schedule: the half-size path (no deferred record in this
+    seeded batch) and the full-length verdict every deferred record takes."""
+    import bench
+    n = 32
+    pk, sig, blob, off = _signed_batch(n, 3)
+    ok, c, nd = _run_mode(hc, pk, sig, blob, off, False)
+    assert ok.all() and nd == 0
     assert int(c[1]) == int(bench.W_SQ_PER_VERIFY * n)
-    # decompression multiplies by sqrt(-1) for about half of all keys
-    assert (bench.W_MUL_PER_VERIFY - 0.5) * n <= int(c[0]) <= (bench.W_MUL_PER_VERIFY + 0.5) * n
+    # the decompressions of -A and -R each multiply by sqrt(-1) for about half of all points
+    assert abs(int(c[0]) / n - bench.W_MUL_PER_VERIFY) <= 0.5
     assert int(c[4]) == 3 * n  # SHA-512 blocks for |R||A||M| = 320 B
+    assert int(c[5]) == 2 * n  # h mod L, d S mod L
+    ok, c, nd = _run_mode(hc, pk, sig, blob, off, True)
+    assert ok.all() and nd == n
+    assert int(c[1]) == int(bench.W_SQ_FULL * n)
+    assert abs(int(c[0]) / n - bench.W_MUL_FULL) <= 0.5
+
+
+def test_op_counts_pin_grouped_constants(hc):
+    """PV_CURVE_MODE=grouped: groups of CURVE_K = 4 signatures share the final inversion."""
+    import bench
+    n = 16
+    pk, sig, blob, off = _signed_batch(n, 4)
+    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())
+    hc.hc_reset_counts()
+    v = np.zeros(n, np.uint8)
+    b = orc.padded(blob)
+    hc.hc_verify_batch_grouped(_p(pk), _p(sig), _p(b), _p(off), ctypes.c_uint64(n), _p(v))
+    c, bad = counts(hc)
+    assert bad == 0 and v.all()
+    assert int(c[1]) == int(bench.W_SQ_GROUPED * n)
+    assert abs(int(c[0]) / n - bench.W_MUL_GROUPED) <= 0.5
+
+
+def test_half_and_full_paths_agree_on_fixtures(hc, raw_vectors, adversarial):
+    """Every fixture verdict through the half-size path AND with every record
+    forced through the full-length verdict (the two code paths of k_curve_half)."""
+    r = raw_vectors
+    sel = np.arange(0, len(r['verdict']), 3)
+    msgs = [r['blob'][int(r['off'][i]):int(r['off'][i + 1])].tobytes() for i in sel]
+    off = np.zeros(len(sel) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    blob = np.frombuffer(b''.join(msgs), np.uint8)
+    want = r['verdict'][sel].astype(bool)
+    for force in (False, True):
+        got, _, nd = _run_mode(hc, r['pk'][sel], r['sig'][sel], blob, off, force)
+        assert (got == want).all()
+    pk, sig, blob, off, want = _adv_arrays(adversarial)
+    for force in (False, True):
+        got, _, nd = _run_mode(hc, pk, sig, blob, off, force)
+        assert (got == want).all()
+
+
+L8 = 8 * L
+PAT33 = int('8' * 33, 16)
+
+
+def _half(hc, h):
+    c = ctypes.create_string_buffer(20)
+    d = ctypes.create_string_buffer(20)
+    neg = ctypes.c_uint32()
+    st = hc.hc_half_scalars(h.to_bytes(32, 'little'), c, d, ctypes.byref(neg))
+    return st, int.from_bytes(c.raw, 'little'), int.from_bytes(d.raw, 'little'), neg.value
+
+
+def test_half_scalars_lattice_properties(hc):
+    """c == d h (mod 8L), d odd and positive, |c| + 0x88..8 and d + 0x88..8 < 2^132
+    (33 signed radix-16 digits) for every HS_HALF result; edge values of h; and
+    the deferral rate of random h stays at the simulated ~0.2 %."""
+    rnd = random.Random(17)
+    cases = [0, 1, 2, 3, 8, L - 1, L - 2, 2 ** 128 - 1, 2 ** 128, 2 ** 128 + 1, 2 ** 252, L // 2, L // 3,
+             (2 ** 252) // 7, 2 ** 200 + 3] + [rnd.randrange(L) for _ in range(4000)]
+    deferred = 0
+    for h in cases:
+        st, c, d, neg = _half(hc, h)
+        assert st in (1, 2)
+        if st == 2:
+            deferred += 1
+            continue
+        cs = -c if neg else c
+        assert d % 2 == 1 and d > 0, h
+        assert (cs - d * h) % L8 == 0, h
+        assert c + PAT33 < 2 ** 132 and d + PAT33 < 2 ** 132, h
+    assert _half(hc, 0)[0] == 1 and _half(hc, 5)[0] == 1   # tiny h: c = h, d = 1
+    assert deferred / len(cases) < 0.01
+
+
+def test_sc_mul_small_vs_bigint(hc):
+    rnd = random.Random(23)
+    out = ctypes.create_string_buffer(32)
+    for _ in range(300):
+        d = rnd.randrange(2 ** 132)
+        s = rnd.randrange(L)
+        hc.hc_sc_mul_small(d.to_bytes(20, 'little'), s.to_bytes(32, 'little'), out)
+        assert int.from_bytes(out.raw, 'little') == (d * s) % L
 
 
 def test_asan_ubsan_run(adversarial):

@@ -69,10 +69,64 @@ static void ensure_btab() {
 
 extern "C" {
 
-// verdicts with exactly the kernel's algorithm; the message blob must have
-// >= 16 readable bytes after the last message (same contract as the kernel)
+// verdicts with exactly the generic kernels' algorithm (k_hash, k_lattice,
+// k_curve_half with its full-length tasks for deferred records); the message
+// blob must have >= 16 readable bytes after the last message (same contract
+// as the kernel).  force_full: every record deferred (PV_CURVE_MODE=full).
+// n_deferred (may be NULL) receives the number of full-length verdicts.
+void hc_verify_batch_mode(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
+                          uint8_t* verdict, int force_full, uint64_t* n_deferred) {
+  ensure_btab();
+  static uint32_t lane[HALF_LANE_WORDS];
+  uint32_t rec[HREC_WORDS];
+  uint64_t nd = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t h[16];
+    const bool pre = hash_one(h, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+    const uint32_t st = lattice_one(rec, pre, h, sig + 64 * i, force_full != 0);
+    bool ok = false;
+    if (st == HS_HALF) {
+      ok = curve_half(pk + 32 * i, sig + 64 * i, rec, lane, g_btab, g_btab + 2 * BT_ENTRIES * BT_WORDS);
+    } else if (st == HS_DEFER) {
+      ok = verify_full_one(pk + 32 * i, sig + 64 * i, h, lane, g_btab);
+      ++nd;
+    }
+    verdict[i] = ok ? 1 : 0;
+  }
+  if (n_deferred) *n_deferred = nd;
+}
+
 void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
                      uint8_t* verdict) {
+  hc_verify_batch_mode(pk, sig, blob, off, n, verdict, 0, nullptr);
+}
+
+// half-size scalars of h (32 LE bytes, < L): |c|, d as 20 LE bytes each
+// (plain values, no digit offset); returns HS_HALF / HS_DEFER
+uint32_t hc_half_scalars(const uint8_t* h32, uint8_t* c20, uint8_t* d20, uint32_t* c_neg) {
+  uint32_t h[8], c[HS_WORDS], d[HS_WORDS];
+  memcpy(h, h32, 32);
+  bool neg = false;
+  const uint32_t st = half_scalars(c, d, neg, h);
+  memcpy(c20, c, 4 * HS_WORDS);
+  memcpy(d20, d, 4 * HS_WORDS);
+  *c_neg = neg ? 1u : 0u;
+  return st;
+}
+
+// s' = d * S mod L (d: 20 LE bytes, S: 32 LE bytes)
+void hc_sc_mul_small(const uint8_t* d20, const uint8_t* s32, uint8_t* out32) {
+  uint32_t d[HS_WORDS], S[8], r[8];
+  memcpy(d, d20, 4 * HS_WORDS);
+  memcpy(S, s32, 32);
+  sc_mul_small(r, d, S);
+  memcpy(out32, r, 32);
+}
+
+// the previous generic schedule: full-length scalars, CURVE_K signatures per
+// lane sharing one inversion (the keyed kernel keeps this group structure)
+void hc_verify_batch_grouped(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                             uint64_t n, uint8_t* verdict) {
   ensure_btab();
   static uint32_t lane[LANE_WORDS];
   uint32_t* h = (uint32_t*)calloc(n ? n * 16 : 16, sizeof(uint32_t));
