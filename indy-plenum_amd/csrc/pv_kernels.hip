@@ -21,6 +21,13 @@ namespace pv {
 // waves per SIMD the curve kernel is compiled for (register budget 512 / w);
 // its hot Horner loop needs ~165 VGPRs; 2 waves/SIMD (<= 256 VGPRs) measured
 // fastest (tools/variant_bench.py: 2 > 3 > 4 waves once spills appear)
+#ifndef PV_HALF_LS
+// lane interleave of k_curve_half's per-lane tables: 1 = lane-contiguous (the
+// compiler loads a field element with dwordx4/x2); 64 = [word][lane] measured
+// 40 % slower (10 dword loads + address arithmetic per field element,
+// tools/variant_bench.py, profiles/r01_ab_layout.json)
+#define PV_HALF_LS 1
+#endif
 #ifndef PV_CURVE_WAVES
 #define PV_CURVE_WAVES 2
 #endif
@@ -235,7 +242,10 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
   }
   __syncthreads();
   const int lane = (int)(threadIdx.x & 63u);
-  uint32_t* scr = scratch + ((uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x) * HALF_LANE_WORDS;
+  // per-lane tables interleaved by PV_HALF_LS lanes ([word][lane] inside each
+  // group of PV_HALF_LS consecutive lanes): coalesced table loads
+  const uint64_t gl = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
+  uint32_t* scr = scratch + (gl / PV_HALF_LS) * (uint64_t)(HALF_LANE_WORDS * PV_HALF_LS) + gl % PV_HALF_LS;
   const uint64_t nd = *dcount;
   const uint64_t full_tasks = (nd + 63) / 64;
   const uint64_t all_tasks = full_tasks + (n + 63) / 64;
@@ -248,7 +258,7 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
       const uint64_t j = t * 64 + lane;
       if (j < nd) {
         const uint64_t i = dlist[j];
-        const bool ok = verify_full_one(pk + 32 * i, sig + 64 * i, dig + 16 * i, scr, btab);
+        const bool ok = verify_full_one<PV_HALF_LS>(pk + 32 * i, sig + 64 * i, dig + 16 * i, scr, btab);
         verdict[i] = ok ? 1 : 0;
         if (ok) atomicOr(&bitmap[i >> 6], 1ull << (i & 63));
       }
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
       uint32_t st = HS_NONE;
       if (i < n) st = rec[HREC_WORDS * i + HREC_FLAGS] & 0xffu;
       bool ok = false;
-      if (st == HS_HALF) ok = curve_half(pk + 32 * i, sig + 64 * i, rec + HREC_WORDS * i, scr, btab, btab + TW);
+      if (st == HS_HALF) ok = curve_half<PV_HALF_LS>(pk + 32 * i, sig + 64 * i, rec + HREC_WORDS * i, scr, btab, btab + TW);
       const uint64_t ball = __ballot(ok);
       if (i < n && st != HS_DEFER) verdict[i] = ok ? 1 : 0;
       if (lane == 0 && ball) atomicOr(&bitmap[t - full_tasks], (unsigned long long)ball);

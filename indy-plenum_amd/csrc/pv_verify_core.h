@@ -197,25 +197,33 @@ PV_HD bool hash_one(uint32_t dig[16], const uint8_t* pk, const uint8_t* sig, con
 }
 
 // ------------------------------------------------------------ table access
+// Per-lane tables (cached multiples of -A / -R) take a word stride S: S = 1
+// is a lane-contiguous table; S = 64 interleaves the 64 lanes of a wavefront
+// word by word ([word][lane]), so one load instruction of the wave reads 256
+// contiguous bytes instead of touching 64 scattered cache lines.
+template <int S = 1>
 PV_HD void store_fe(uint32_t* p, const fe& f) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) p[i] = f.v[i];
+  for (int i = 0; i < 10; ++i) p[i * S] = f.v[i];
 }
+template <int S = 1>
 PV_HD void load_fe(fe& f, const uint32_t* p) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) f.v[i] = p[i];
+  for (int i = 0; i < 10; ++i) f.v[i] = p[i * S];
 }
+template <int S = 1>
 PV_HD void store_cached(uint32_t* p, const ge_cached& c) {
-  store_fe(p, c.YpX);
-  store_fe(p + 10, c.YmX);
-  store_fe(p + 20, c.Z2);
-  store_fe(p + 30, c.T2d);
+  store_fe<S>(p, c.YpX);
+  store_fe<S>(p + 10 * S, c.YmX);
+  store_fe<S>(p + 20 * S, c.Z2);
+  store_fe<S>(p + 30 * S, c.T2d);
 }
+template <int S = 1>
 PV_HD void load_cached(ge_cached& c, const uint32_t* p) {
-  load_fe(c.YpX, p);
-  load_fe(c.YmX, p + 10);
-  load_fe(c.Z2, p + 20);
-  load_fe(c.T2d, p + 30);
+  load_fe<S>(c.YpX, p);
+  load_fe<S>(c.YmX, p + 10 * S);
+  load_fe<S>(c.Z2, p + 20 * S);
+  load_fe<S>(c.T2d, p + 30 * S);
 }
 PV_HD void load_niels(ge_niels& q, const uint32_t* p) {
   load_fe(q.ypx, p);
@@ -281,17 +289,18 @@ PV_HD void btable_entry(uint32_t* p, int k, int q = 0) {
 // by choosing WHICH of Y+X / Y-X to load and negating the C term, so no
 // 10-limb copies are made: this keeps the hot loop inside 3 waves/SIMD of
 // registers.  Same formulas as ge_add_cached / ge_madd (add-2008-hwcd-3).
+template <int S = 1>
 PV_HD void ge_add_cached_at(ge_p1p1& r, const ge_p3& p, const uint32_t* q, bool neg) {
   fe c, d, a, b, u, g;
-  load_fe(g, q + 30);             // 2d*T2
+  load_fe<S>(g, q + 30 * S);             // 2d*T2
   fe_mul(c, g, p.T);
-  load_fe(g, q + 20);             // 2*Z2
+  load_fe<S>(g, q + 20 * S);             // 2*Z2
   fe_mul(d, p.Z, g);
   fe_add(u, p.Y, p.X);
-  load_fe(g, q + (neg ? 10 : 0)); // Y2+X2 (Y2-X2 for -Q)
+  load_fe<S>(g, q + (neg ? 10 * S : 0)); // Y2+X2 (Y2-X2 for -Q)
   fe_mul(a, u, g);
   fe_sub(u, p.Y, p.X);
-  load_fe(g, q + (neg ? 0 : 10));
+  load_fe<S>(g, q + (neg ? 0 : 10 * S));
   fe_mul(b, u, g);
   fe_sub(r.X, a, b);
   fe_add(r.Y, a, b);
@@ -323,23 +332,24 @@ PV_HD void ge_madd_at(ge_p1p1& r, const ge_p3& p, const uint32_t* q, bool neg) {
 
 // ----------------------------------------------------------------- curve
 // cached multiples 0..8 of P into a per-lane table (9 x 40 words)
+template <int LS = 1>
 PV_HD void build_atab(uint32_t* atab, const ge_p3& P) {
   ge_cached c;
   ge_cached_identity(c);
-  store_cached(atab, c);
+  store_cached<LS>(atab, c);
   ge_p3_to_cached(c, P);
-  store_cached(atab + AT_ENTRY, c);
+  store_cached<LS>(atab + AT_ENTRY * LS, c);
   ge_p3 prev = P;
 #pragma unroll 1
   for (int k = 2; k <= 8; ++k) {
     // re-read 1*P from the table instead of keeping it live (register budget)
     ge_cached c1;
-    load_cached(c1, atab + AT_ENTRY);
+    load_cached<LS>(c1, atab + AT_ENTRY * LS);
     ge_p1p1 t;
     ge_add_cached(t, prev, c1, false);
     ge_p1p1_to_p3(prev, t);
     ge_p3_to_cached(c, prev);
-    store_cached(atab + AT_ENTRY * k, c);
+    store_cached<LS>(atab + AT_ENTRY * k * LS, c);
   }
 }
 
@@ -347,6 +357,7 @@ PV_HD void build_atab(uint32_t* atab, const ge_p3& P) {
 // [-8, 8); ss + 0x8080..80 gives radix-256 digits (byte - 128) in [-128, 128);
 // hh, ss < 2^253 so neither addition overflows 2^256.  Horner from the top:
 // per window 4 doublings, one A add, and a B add on even windows.
+template <int LS = 1>
 PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss[8], const uint32_t* atab,
                              const uint32_t* btab) {
   uint32_t hp[8], sp[8];
@@ -363,7 +374,7 @@ PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss
   uint32_t hw = hp[7], sw = sp[7];
   {
     const int dA = (int)(hw >> 28) - 8;
-    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
+    ge_add_cached_at<LS>(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
     ge_p1p1_to_p2(r2, t);
   }
 #pragma unroll 1
@@ -385,11 +396,7 @@ PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss
     ge_p2_dbl(t, r2);
     ge_p1p1_to_p3(acc, t);
     const int dA = (int)((hw >> (4 * (i & 7))) & 15u) - 8;
-#ifdef PV_EXPERIMENT_FIXED_ENTRY   // timing experiment only: wrong verdicts, measures the table-fetch cost
-    ge_add_cached_at(t, acc, atab + AT_ENTRY, dA < 0);
-#else
-    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
-#endif
+    ge_add_cached_at<LS>(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
     if ((i & 1) == 0) {
       const int dB = (int)((sw >> (8 * ((i >> 1) & 3))) & 255u) - 128;
       ge_p1p1_to_p3(acc, t);
@@ -405,6 +412,7 @@ PV_HD void double_scalarmult(ge_p2& out, const uint32_t hh[8], const uint32_t ss
 // kernel).  Inputs are loaded right where they are consumed so that no
 // 32-byte value stays live across the whole verification (register budget of
 // the hot loop).  false = rejected before the final comparison.
+template <int LS = 1>
 PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const uint32_t* dig_src, uint32_t* atab,
                        const uint32_t* btab) {
   ge_p3 negA;
@@ -413,7 +421,7 @@ PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const u
     load8(A, pk);
     if (!ge_frombytes_negate(negA, A)) return false;
   }
-  build_atab(atab, negA);
+  build_atab<LS>(atab, negA);
   uint32_t hh[8], S[8];
   {
     uint32_t dig[16];
@@ -422,7 +430,7 @@ PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const u
     sc_reduce64(hh, dig);  // h = SHA-512(R||A||M) mod L (App. C.2 step 5)
   }
   load8(S, sig + 32);
-  double_scalarmult(rp, hh, S, atab, btab);
+  double_scalarmult<LS>(rp, hh, S, atab, btab);
   return true;
 }
 
@@ -740,6 +748,7 @@ PV_HD uint32_t lattice_one(uint32_t* rec, bool pre, const uint32_t* dig, const u
 // 2^128 B (high 16 bytes), both added on even windows.  Horner from the top:
 // per window 4 doublings, one add from each per-lane table, and on even
 // windows two base-point adds.  Leaves the last sum in p1p1 form.
+template <int LS = 1>
 PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const uint32_t* rtab, const uint32_t* blo,
                     const uint32_t* bhi) {
   uint32_t cp[4], dp[4], sl[4], sh[4];
@@ -755,10 +764,10 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
   ge_p3_0(acc);
   {
     const int dA = (int)(rec[HREC_C + 4] & 15u) - 8;
-    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
+    ge_add_cached_at<LS>(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
     ge_p1p1_to_p3(acc, t);
     const int dR = (int)(rec[HREC_D + 4] & 15u) - 8;
-    ge_add_cached_at(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY, dR < 0);
+    ge_add_cached_at<LS>(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY * LS, dR < 0);
     ge_p1p1_to_p2(r2, t);
   }
   uint32_t cw = cp[3], dw = dp[3], lw = sl[3], hw = sh[3];
@@ -787,10 +796,10 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
     ge_p1p1_to_p3(acc, t);
     const int sh4 = 4 * (w & 7);
     const int dA = (int)((cw >> sh4) & 15u) - 8;
-    ge_add_cached_at(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY, dA < 0);
+    ge_add_cached_at<LS>(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
     ge_p1p1_to_p3(acc, t);
     const int dR = (int)((dw >> sh4) & 15u) - 8;
-    ge_add_cached_at(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY, dR < 0);
+    ge_add_cached_at<LS>(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY * LS, dR < 0);
     if ((w & 1) == 0) {
       const int sh8 = 8 * ((w >> 1) & 3);
       const int dL = (int)((lw >> sh8) & 255u) - 128;
@@ -816,7 +825,9 @@ PV_HD bool p1p1_is_identity(const ge_p1p1& p) {
 // The half-size verdict for a HS_HALF record (see pv_lattice.h):
 // accept iff -A and -R decode and s' B + c (-A) + d (-R) == O.  R's y must be
 // canonical (a non-canonical R never equals an encoding libsodium computes).
-// scratch = HALF_LANE_WORDS words of this lane; blo/bhi = tables of B, 2^128 B.
+// scratch = HALF_LANE_WORDS words of this lane (word stride LS); blo/bhi =
+// tables of B, 2^128 B.
+template <int LS = 1>
 PV_HD bool curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, uint32_t* scratch,
                       const uint32_t* blo, const uint32_t* bhi) {
   ge_p3 P;
@@ -831,24 +842,25 @@ PV_HD bool curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* rec
     fe_neg(P.T, P.T);
     fe_carry(P.T);
   }
-  build_atab(scratch, P);
+  build_atab<LS>(scratch, P);
   {
     uint32_t R[8];
     load8(R, sig);
     if (!y_is_canonical(R) || !ge_frombytes_negate(P, R)) return false;  // -R
   }
-  build_atab(scratch + AT_WORDS, P);
+  build_atab<LS>(scratch + AT_WORDS * LS, P);
   ge_p1p1 t;
-  msm_half(t, rec, scratch, scratch + AT_WORDS, blo, bhi);
+  msm_half<LS>(t, rec, scratch, scratch + AT_WORDS * LS, blo, bhi);
   return p1p1_is_identity(t);
 }
 
 // Full-length verdict of one signature (deferred records): R' = h(-A) + S B,
-// encode, compare.  scratch = AT_WORDS words; btab = table of B.
+// encode, compare.  scratch = AT_WORDS words (stride LS); btab = table of B.
+template <int LS = 1>
 PV_HD bool verify_full_one(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, uint32_t* scratch,
                            const uint32_t* btab) {
   ge_p2 rp;
-  if (!curve_point(rp, pk, sig, dig, scratch, btab)) return false;
+  if (!curve_point<LS>(rp, pk, sig, dig, scratch, btab)) return false;
   uint32_t enc[8], R[8];
   ge_p2_tobytes(enc, rp);
   load8(R, sig);

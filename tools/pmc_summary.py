@@ -49,8 +49,11 @@ def main(d):
         if 'GRBM_GUI_ACTIVE' in c:
             e['gpu_cycles_per_xcd'] = c['GRBM_GUI_ACTIVE'] / 8
         out['kernels'][k] = e
-    curve = next((v for k, v in out['kernels'].items() if k.startswith('pv::k_curve') and 'true' not in k), {})
-    out['hbm_bytes_per_launch'] = curve.get('hbm_bytes_per_launch')
+    # the generic batches' curve kernel: k_curve_half (default), else the grouped k_curve<false>
+    names = sorted(out['kernels'], key=lambda k: not k.startswith('pv::k_curve_half'))
+    curve_k = next((k for k in names if k.startswith('pv::k_curve') and 'true' not in k), None)
+    out['curve_kernel'] = curve_k
+    out['hbm_bytes_per_launch'] = out['kernels'].get(curve_k, {}).get('hbm_bytes_per_launch')
     print(json.dumps(out, indent=1))
 
 
