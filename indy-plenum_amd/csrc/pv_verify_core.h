@@ -117,11 +117,39 @@ PV_HD uint32_t funnel32(uint32_t hi, uint32_t lo, uint32_t sh) {
 // message byte offset of block `blk` of R || A || M (block 0 holds R || A and M[0, 64))
 PV_HD uint64_t hram_q(uint64_t blk) { return blk == 0 ? 0 : 128 * blk - 64; }
 
-// Raw aligned words covering message bytes [q, q + 128): one guarded load per
-// word that holds a message byte (the blob only needs the usual 16 readable
-// bytes after the last message).  Split from the assembly so the hash kernel
-// can issue the next block's loads before compressing the current one.
-PV_HD void msg_fetch(uint32_t y[33], const uint8_t* m, uint64_t mlen, uint64_t q) {
+// Raw aligned words covering message bytes [q, q + 128), fetched as 4-word
+// groups: group g is loaded iff its first word holds a message byte, so a
+// group reads at most 15 bytes past the message end (the blob guarantees 16
+// readable bytes after the last message) and each lane issues <= 9 dwordx4
+// loads instead of 33 guarded dword loads.  Block 0 only needs words 0..16
+// (M[0, 64) behind R || A).  Words past the message are masked by
+// msg_assemble.  The pointer keeps the blob's address space (global loads).
+#ifndef PV_FETCH_WORDS
+constexpr int MSG_Y = 36;
+PV_HD void msg_fetch(uint32_t y[MSG_Y], const uint8_t* m, uint64_t mlen, uint64_t q, bool first) {
+  const int64_t rem = (int64_t)mlen - (int64_t)q;
+  const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + q) & 3u);
+  const uint32_t* wp = reinterpret_cast<const uint32_t*>(m + q - mis);
+#pragma unroll
+  for (int g = 0; g < 9; ++g) {
+    const bool ld = (int64_t)(16 * g) - (int64_t)mis < rem && (!first || g < 5);
+    uint32_t a = 0, b = 0, c = 0, d = 0;
+    if (ld) {
+      a = wp[4 * g];
+      b = wp[4 * g + 1];
+      c = wp[4 * g + 2];
+      d = wp[4 * g + 3];
+    }
+    y[4 * g] = a;
+    y[4 * g + 1] = b;
+    y[4 * g + 2] = c;
+    y[4 * g + 3] = d;
+  }
+}
+#else
+// (A/B baseline) one guarded dword load per word that holds a message byte
+constexpr int MSG_Y = 33;
+PV_HD void msg_fetch(uint32_t y[MSG_Y], const uint8_t* m, uint64_t mlen, uint64_t q, bool) {
   const int64_t rem = (int64_t)mlen - (int64_t)q;
   const uintptr_t base = reinterpret_cast<uintptr_t>(m) + q;
   const uint32_t mis = (uint32_t)(base & 3u);
@@ -129,10 +157,11 @@ PV_HD void msg_fetch(uint32_t y[33], const uint8_t* m, uint64_t mlen, uint64_t q
 #pragma unroll
   for (int k = 0; k < 33; ++k) y[k] = (int64_t)(4 * k) - (int64_t)mis < rem ? wp[k] : 0u;
 }
+#endif
 
 // 32 little-endian words = message bytes [q, q + 128) with SHA padding applied:
 // bytes past mlen are zero and byte mlen is 0x80 (funnel shift of the raw words)
-PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[33], const uint8_t* m, uint64_t mlen, uint64_t q) {
+PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[MSG_Y], const uint8_t* m, uint64_t mlen, uint64_t q) {
   const int64_t rem = (int64_t)mlen - (int64_t)q;
   const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + q) & 3u);
 #pragma unroll
@@ -149,7 +178,7 @@ PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[33], const uint8_t* m, 
 
 // block `blk` of R || A || M as 16 big-endian 64-bit words from the raw message
 // words of hram_q(blk) (R, A read from sig/pk on block 0; length words on the last)
-PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[33], const uint8_t* sig, const uint8_t* pk,
+PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[MSG_Y], const uint8_t* sig, const uint8_t* pk,
                          const uint8_t* m, uint64_t mlen, uint64_t blk, uint64_t nblk) {
   const bool first = blk == 0;
   uint32_t x[32];
@@ -175,8 +204,8 @@ PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[33], const uint8_t* si
 
 PV_HD void hram_block(uint64_t w[16], const uint8_t* sig, const uint8_t* pk, const uint8_t* m, uint64_t mlen,
                       uint64_t blk, uint64_t nblk) {
-  uint32_t y[33];
-  msg_fetch(y, m, mlen, hram_q(blk));
+  uint32_t y[MSG_Y];
+  msg_fetch(y, m, mlen, hram_q(blk), blk == 0);
   hram_assemble(w, y, sig, pk, m, mlen, blk, nblk);
 }
 
