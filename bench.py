@@ -70,11 +70,12 @@ W_MAD_FULL = int(W_MUL_FULL * 100 + W_SQ_FULL * 55)
 # sharing one inversion (3 of every 4 254-squaring inversions become 3 multiplies)
 W_MUL_GROUPED, W_SQ_GROUPED = 1581.5, 1326.5
 W_MAD_GROUPED = int(W_MUL_GROUPED * 100 + W_SQ_GROUPED * 55)
-# keyed batches (prepared keys, 4-way comb of -A): 60 doublings instead of 256,
-# no decompression; decompression, the comb tables (3 x 61 doublings, 32 affine
-# multiples, one shared inversion) run once per distinct key in k_keys
-W_MUL_KEYED, W_SQ_KEYED = 858.0, 303.5
-W_MUL_KEYPREP, W_SQ_KEYPREP = 1031.0, 1241.0
+# keyed batches (prepared keys, 8-way comb of -A over the 32-bit words of h):
+# 28 doublings instead of 253, no decompression; decompression and the comb
+# tables (7 x 29 doublings, 64 affine multiples, one shared inversion) run once
+# per distinct key in k_keys
+W_MUL_KEYED, W_SQ_KEYED = 762.0, 175.5
+W_MUL_KEYPREP, W_SQ_KEYPREP = 1547.5, 1321.0
 W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
 # v_mad_u64_u32 issue ceiling of one MI355X measured by tools/ubench/mad_peak.hip
 # (profiles/r01_mad_peak.json, best over 1..8 waves/SIMD): lane-ops/s, whole chip.

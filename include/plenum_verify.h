@@ -65,10 +65,10 @@ extern "C" {
  * Verdicts are identical; only the work changes. */
 #define PV_FLAG_DEDUP_KEYS 1u
 
-/* words per prepared key (pv_keys_prepare_device): a 4-way comb of -A —
- * affine multiples k * 2^(64 q) * (-A), k = 0..8, q = 0..3, 32 words each —
+/* words per prepared key (pv_keys_prepare_device): an 8-way comb of -A —
+ * affine multiples k * 2^(32 q) * (-A), k = 0..8, q = 0..7, 32 words each —
  * + status word (+ padding) */
-#define PV_KEY_WORDS 1160u
+#define PV_KEY_WORDS 2312u
 
 /* Initialise the engine on the GPUs in device_mask (bit d = HIP device d;
  * 0 = all visible devices).  Idempotent.  Builds the base-point table. */
@@ -102,8 +102,8 @@ int pv_verify_batch_device(const uint8_t *pk, const uint8_t *sig, const uint8_t 
 /* Verifying-key cache on the device.  pv_keys_prepare_device fills ktab
  * (k x PV_KEY_WORDS words) for the k 32-byte keys in pk; a key that libsodium
  * would refuse (non-canonical, small order, not on the curve) is marked so and
- * every signature under it is rejected.  The table is a 4-way comb, so a
- * keyed verification needs 60 doublings instead of 256.  pv_verify_keyed_device verifies n
+ * every signature under it is rejected.  The table is an 8-way comb, so a
+ * keyed verification needs 28 doublings instead of 253.  pv_verify_keyed_device verifies n
  * signatures whose key is pk[key_idx[i]] (the same pk array the table was built
  * from: the hash still covers the key's bytes) — same verdicts as
  * pv_verify_batch_device on the gathered keys, without re-decompressing a key

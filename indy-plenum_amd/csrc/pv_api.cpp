@@ -126,7 +126,7 @@ int init_device(Device& d) {
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d.id));
   d.cu_count = prop.multiProcessorCount;
-  HIP_OK(d.btab.ensure(pv::BTAB_QUARTERS * pv::BTAB_ENTRIES * pv::BTAB_WORDS));
+  HIP_OK(d.btab.ensure(pv::BTAB_CHUNKS * pv::BTAB_ENTRIES * pv::BTAB_WORDS));
   HIP_OK(pv::launch_btable_init(d.btab.p, d.stream));
   // persistent curve grid: resident blocks per CU from the occupancy query
   // (kept <= 4 blocks of 256 threads per CU, see cdna_hip_programming.md §1)

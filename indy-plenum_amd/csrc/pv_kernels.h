@@ -10,7 +10,7 @@ namespace pv {
 // base-point table: 129 niels entries (k*B, k = 0..128), 32 words each
 constexpr int BTAB_ENTRIES = 129;
 constexpr int BTAB_WORDS = 32;
-constexpr int BTAB_QUARTERS = 4;   // tables for 2^(64 q) B, q = 0..3 (comb kernel of prepared keys)
+constexpr int BTAB_CHUNKS = 8;     // tables for 2^(32 q) B, q = 0..7 (comb kernel of prepared keys)
 // per-lane scratch: A table (9 cached entries k*(-A), 40 words each) + the
 // CURVE_K points awaiting the shared inversion (40 words each)
 constexpr int ATAB_WORDS = 9 * 40 + 4 * 40;
@@ -63,10 +63,10 @@ hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32
                              uint64_t* bitmap, uint64_t n, const uint32_t* dlist, const unsigned long long* dcount,
                              unsigned long long* tasks, int blocks, hipStream_t s);
 
-// prepared keys: KEYTAB_WORDS words per key (4 comb tables of affine multiples
-// k * 2^(64 q) * (-A) + status); KEYTAB_SCRATCH words of scratch per key
-constexpr int KEYTAB_WORDS = 4 * 9 * 32 + 8;
-constexpr int KEYTAB_SCRATCH = 32 * 10;
+// prepared keys: KEYTAB_WORDS words per key (8 comb tables of affine multiples
+// k * 2^(32 q) * (-A) + status); KEYTAB_SCRATCH words of scratch per key
+constexpr int KEYTAB_WORDS = 8 * 9 * 32 + 8;
+constexpr int KEYTAB_SCRATCH = 64 * 10;
 hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
 
 // keygen + sign: pk[i], sig[i] for seed[i] over M_i

@@ -33,7 +33,7 @@ namespace pv {
 #endif
 
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
-                  KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && COMB_Q == BTAB_QUARTERS &&
+                  KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && BT_CHUNKS == BTAB_CHUNKS &&
                   HREC_WORDS == HSREC_WORDS && HALF_LANE_WORDS == HALF_SCRATCH_WORDS,
               "table layout");
 
@@ -120,14 +120,14 @@ hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blo
 }
 
 // ---------------------------------------------------------- base-point table
-// BTAB_QUARTERS tables, q-major: entry k of table q = k * 2^(64 q) * B
+// BTAB_CHUNKS tables, q-major: entry k of table q = k * 2^(32 q) * B
 __global__ void k_btable_init(uint32_t* btab) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < BTAB_QUARTERS * BTAB_ENTRIES) btable_entry(btab + g * BTAB_WORDS, g % BTAB_ENTRIES, g / BTAB_ENTRIES);
+  if (g < BTAB_CHUNKS * BTAB_ENTRIES) btable_entry(btab + g * BTAB_WORDS, g % BTAB_ENTRIES, g / BTAB_ENTRIES);
 }
 
 hipError_t launch_btable_init(uint32_t* btab, hipStream_t s) {
-  const int n = BTAB_QUARTERS * BTAB_ENTRIES;
+  const int n = BTAB_CHUNKS * BTAB_ENTRIES;
   hipLaunchKernelGGL(k_btable_init, dim3((n + 63) / 64), dim3(64), 0, s, btab);
   return hipGetLastError();
 }
@@ -148,16 +148,18 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
                                                                         uint64_t* __restrict__ bitmap, uint64_t n,
                                                                         const uint32_t* __restrict__ ktab,
                                                                         const uint32_t* __restrict__ kidx) {
-  // generic kernel: table q = 0 (16.5 KB); comb kernel of prepared keys: all 4 (66 KB)
-  constexpr int BT_LDS_WORDS = (KEYED ? BTAB_QUARTERS : 1) * BTAB_ENTRIES * BTAB_WORDS;
+  // generic kernel: table q = 0 (16.5 KB); comb kernel of prepared keys: the
+  // even chunk tables 0, 2, 4, 6 (66 KB; the odd ones are read from global)
+  constexpr int TW = BTAB_ENTRIES * BTAB_WORDS;
+  constexpr int BT_LDS_WORDS = (KEYED ? 4 : 1) * TW;
   __shared__ uint32_t btab[BT_LDS_WORDS];
-  for (int j = threadIdx.x; j < BT_LDS_WORDS; j += CURVE_BLOCK) btab[j] = btab_g[j];
+  for (int j = threadIdx.x; j < BT_LDS_WORDS; j += CURVE_BLOCK) btab[j] = btab_g[(j / TW) * 2 * TW + j % TW];
   __syncthreads();
   const uint64_t nthreads = (uint64_t)gridDim.x * CURVE_BLOCK;
   const uint64_t gid = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
   uint32_t* lane = scratch + gid * LANE_WORDS;
   for (uint64_t base = 0; base < n; base += CURVE_K * nthreads) {
-    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx);
+    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx, btab_g);
 #pragma unroll
     for (int k = 0; k < CURVE_K; ++k) {
       const uint64_t i = base + (uint64_t)k * nthreads + gid;
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
   __shared__ uint32_t btab[2 * TW];
   for (int j = threadIdx.x; j < TW; j += CURVE_BLOCK) {
     btab[j] = btab_g[j];                 // q = 0: B
-    btab[TW + j] = btab_g[2 * TW + j];   // q = 2: 2^128 B
+    btab[TW + j] = btab_g[4 * TW + j];   // q = 4: 2^128 B
   }
   __syncthreads();
   const int lane = (int)(threadIdx.x & 63u);
@@ -311,7 +313,7 @@ hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32
 }
 
 // -------------------------------------------------------------- key cache
-__global__ __launch_bounds__(256) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
+__global__ __launch_bounds__(256, 2) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
                                                uint32_t* __restrict__ scr) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j < k) key_prepare(ktab + j * KEY_WORDS, scr + j * KEY_SCRATCH, pk + 32 * j);

@@ -272,14 +272,15 @@ PV_HD void ge_basepoint(ge_p3& B) {
   fe_neg(B.T, nb.T); fe_carry(B.T);
 }
 
-// niels form of k * 2^(64 q) * B (k <= 255, q = 0..3), written as 32 words.
-// Table q = 0 serves the generic kernel; the comb kernel of prepared keys uses
-// all four (B_q = 2^(64 q) B, so S*B = sum_q S_q B_q with 64-bit S_q).
+// niels form of k * 2^(32 q) * B (k <= 255, q = 0..7), written as 32 words.
+// Table q = 0 serves the generic kernels (q = 4, 2^128 B, the half-size one);
+// the comb kernel of prepared keys uses all eight (B_q = 2^(32 q) B, so
+// S*B = sum_q S_q B_q with the 32-bit words S_q).
 PV_HD void btable_entry(uint32_t* p, int k, int q = 0) {
   ge_p3 B, acc;
   ge_basepoint(B);
 #pragma unroll 1
-  for (int d = 0; d < 64 * q; ++d) {
+  for (int d = 0; d < 32 * q; ++d) {
     ge_p1p1 t;
     ge_p3_dbl(t, B);
     ge_p1p1_to_p3(B, t);
@@ -464,21 +465,25 @@ PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const u
 }
 
 // ------------------------------------------------------------- key cache
-// A verifying key prepared once and shared by every signature under it, as a
-// 4-way comb: A_q = 2^(64 q) * (-A) for q = 0..3, each with its 9 multiples
-// k * A_q (k = 0..8) in AFFINE niels form (y+x, y-x, 2dxy; 32 words per entry,
-// all 32 non-trivial points normalised with one shared inversion).  Then
-//   h*(-A) = sum_q h_q A_q,   S*B = sum_q S_q B_q   (h_q, S_q the 64-bit quarters)
-// and the double-scalar multiplication needs 60 doublings instead of 256.  The
-// group element R' = h(-A) + S B is the same, so the verdict (encode(R') == R)
-// is bit-identical.  Status word: 1 = A canonical,
+// A verifying key prepared once and shared by every signature under it, as an
+// 8-way comb over the 32-bit words of the scalar: A_q = 2^(32 q) * (-A) for
+// q = 0..7, each with its 9 multiples k * A_q (k = 0..8) in AFFINE niels form
+// (y+x, y-x, 2dxy; 32 words per entry, all 64 non-trivial points normalised
+// with one shared inversion).  With the base-point tables B_q = 2^(32 q) B,
+//   h*(-A) = sum_q h_q A_q,   S*B = sum_q S_q B_q   (h_q, S_q = word q)
+// and the double-scalar multiplication needs 28 doublings instead of 253 (the
+// 4-way comb of 64-bit quarters needed 60).  The group element
+// R' = h(-A) + S B is the same, so the verdict (encode(R') == R) is
+// bit-identical.  Status word: 1 = A canonical,
 // not small order, decompresses (steps 2-4).
-constexpr int COMB_Q = 4;
+constexpr int COMB_Q = 8;
+constexpr int BT_CHUNKS = 8;            // base-point tables 2^(32 q) B, q = 0..7
+constexpr int BT_TABLE = BT_ENTRIES * BT_WORDS;
 constexpr int KT_ENTRY = 32;
 constexpr int KT_TABLE = 9 * KT_ENTRY;
 constexpr int KEY_STATUS = COMB_Q * KT_TABLE;
 constexpr int KEY_WORDS = KEY_STATUS + 8;
-constexpr int KEY_SCRATCH = 32 * 10;   // prefix products of the shared inversion
+constexpr int KEY_SCRATCH = 8 * COMB_Q * 10;   // prefix products of the shared inversion
 
 PV_HD void store_xyz(uint32_t* p, const ge_p3& q) {
   store_fe(p, q.X);
@@ -492,8 +497,8 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
   load8(A, pk);
   ge_p3 P;
   const bool ok = y_is_canonical(A) && !has_small_order(A) && ge_frombytes_negate(P, A);
-#pragma unroll 1
-  for (int k = 0; k < KEY_WORDS; ++k) kt[k] = 0;
+  // (only the words the comb reads are written: entries' words 30-31 and the
+  // words after the status are padding)
   kt[KEY_STATUS] = ok ? 1u : 0u;
   if (!ok) return;
   // projective multiples k * A_q (X, Y, Z) into the entry slots
@@ -511,14 +516,14 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
       ge_p1p1_to_p3(Q, t);
       store_xyz(tq + k * KT_ENTRY, Q);
     }
-    if (q + 1 < COMB_Q) {  // A_{q+1} = 2^64 A_q = 2^61 (8 A_q)
+    if (q + 1 < COMB_Q) {  // A_{q+1} = 2^32 A_q = 2^29 (8 A_q)
       ge_p1p1 t;
       ge_p2 r;
       fe_copy(r.X, Q.X);
       fe_copy(r.Y, Q.Y);
       fe_copy(r.Z, Q.Z);
 #pragma unroll 1
-      for (int d = 0; d < 60; ++d) {
+      for (int d = 0; d < 28; ++d) {
         ge_p2_dbl(t, r);
         ge_p1p1_to_p2(r, t);
       }
@@ -526,10 +531,11 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
       ge_p1p1_to_p3(P, t);
     }
   }
-  // one inversion for all 32 Z's (Montgomery's trick; prefix products in scr)
+  // one inversion for all 8 * COMB_Q Z's (Montgomery's trick; prefix products in scr)
+  constexpr int NE = 8 * COMB_Q;
   fe acc, z, u;
 #pragma unroll 1
-  for (int e = 0; e < 32; ++e) {
+  for (int e = 0; e < NE; ++e) {
     const uint32_t* slot = kt + (e >> 3) * KT_TABLE + ((e & 7) + 1) * KT_ENTRY;
     load_fe(z, slot + 20);
     if (e == 0) fe_copy(acc, z);
@@ -540,7 +546,7 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
   fe d2;
   fe_const_d2(d2);
 #pragma unroll 1
-  for (int e = 31; e >= 0; --e) {
+  for (int e = NE - 1; e >= 0; --e) {
     uint32_t* slot = kt + (e >> 3) * KT_TABLE + ((e & 7) + 1) * KT_ENTRY;
     fe zi, x, y;
     if (e > 0) {
@@ -564,62 +570,82 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
     store_fe(slot + 20, u);
   }
   // identity entries (k = 0): y+x = 1, y-x = 1, 2dxy = 0
+  fe one, zero;
+  fe_1(one);
+  fe_0(zero);
 #pragma unroll 1
   for (int q = 0; q < COMB_Q; ++q) {
-    kt[q * KT_TABLE] = 1;
-    kt[q * KT_TABLE + 10] = 1;
+    store_fe(kt + q * KT_TABLE, one);
+    store_fe(kt + q * KT_TABLE + 10, one);
+    store_fe(kt + q * KT_TABLE + 20, zero);
   }
 }
 
-// R' = hh*(-A) + ss*B from a prepared key (4 comb tables in kt) and the four
-// base-point tables (btab4, q-major, BT_ENTRIES x BT_WORDS each).  Windows
-// w = 15..0 (4 doublings apart): per window one affine add per quarter with the
-// signed radix-16 digit 16q + w of hh, and on even windows one per quarter with
-// the signed radix-256 digit 8q + w/2 of ss.  Digit words: 2q + (w >> 3).
+// R' = hh*(-A) + ss*B from a prepared key (8 comb tables in kt) and the eight
+// base-point tables: even chunks in `bl` (chunk 2t at bl + t * BT_TABLE, LDS in
+// the kernel), odd chunks in `bg` (chunk q at bg + q * BT_TABLE, global).
+// Windows w = 7..0 (4 doublings apart): per window one affine add per chunk q
+// with the signed radix-16 digit 8q + w of hh, and on even windows one per
+// chunk with the signed radix-256 digit 4q + w/2 of ss.  The chunk loops are
+// not unrolled (code size); the digit words rotate through static indices.
 PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32_t ss[8], const uint32_t* kt,
-                                  const uint32_t* btab4) {
+                                  const uint32_t* bl, const uint32_t* bg) {
   uint32_t hp[8], sp[8];
   sc_add_pattern(hp, hh, 0x88888888u);
   sc_add_pattern(sp, ss, 0x80808080u);
+  uint32_t se[4], so[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    se[t] = sp[2 * t];
+    so[t] = sp[2 * t + 1];
+  }
   ge_p3 acc;
   ge_p3_0(acc);
   ge_p1p1 t;
   ge_p2 r2;
 #pragma unroll 1
-  for (int half = 1; half >= 0; --half) {
-    uint32_t hw[4], sw[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      hw[q] = half ? hp[2 * q + 1] : hp[2 * q];
-      sw[q] = half ? sp[2 * q + 1] : sp[2 * q];
-    }
+  for (int w = 7; w >= 0; --w) {
+    if (w != 7) {
 #pragma unroll 1
-    for (int i = 7; i >= 0; --i) {
-      if (half == 0 || i != 7) {
-#pragma unroll 1
-        for (int k = 0; k < 3; ++k) {
-          ge_p2_dbl(t, r2);
-          ge_p1p1_to_p2(r2, t);
-        }
+      for (int k = 0; k < 3; ++k) {
         ge_p2_dbl(t, r2);
+        ge_p1p1_to_p2(r2, t);
+      }
+      ge_p2_dbl(t, r2);
+      ge_p1p1_to_p3(acc, t);
+    }
+    const int sh4 = 4 * w;
+    const bool bwin = (w & 1) == 0;
+#pragma unroll 1
+    for (int q = 0; q < COMB_Q; ++q) {
+      const int dA = (int)((hp[0] >> sh4) & 15u) - 8;
+      ge_madd_at(t, acc, kt + q * KT_TABLE + (dA < 0 ? -dA : dA) * KT_ENTRY, dA < 0);
+      if (q + 1 < COMB_Q || bwin) ge_p1p1_to_p3(acc, t);
+      else ge_p1p1_to_p2(r2, t);          // a doubling comes next: no T needed
+      const uint32_t x = hp[0];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) hp[j] = hp[j + 1];
+      hp[7] = x;
+    }
+    if (bwin) {
+      const int sh8 = 8 * (w >> 1);
+#pragma unroll 1
+      for (int u = 0; u < 4; ++u) {   // even chunks 0, 2, 4, 6
+        const int dB = (int)((se[0] >> sh8) & 255u) - 128;
+        ge_madd_at(t, acc, bl + u * BT_TABLE + (dB < 0 ? -dB : dB) * BT_WORDS, dB < 0);
         ge_p1p1_to_p3(acc, t);
+        const uint32_t x = se[0];
+        se[0] = se[1]; se[1] = se[2]; se[2] = se[3]; se[3] = x;
       }
-      const bool bwin = (i & 1) == 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int dA = (int)((hw[q] >> (4 * i)) & 15u) - 8;
-        ge_madd_at(t, acc, kt + q * KT_TABLE + (dA < 0 ? -dA : dA) * KT_ENTRY, dA < 0);
-        if (q < 3 || bwin) ge_p1p1_to_p3(acc, t);
+#pragma unroll 1
+      for (int u = 0; u < 4; ++u) {   // odd chunks 1, 3, 5, 7
+        const int dB = (int)((so[0] >> sh8) & 255u) - 128;
+        ge_madd_at(t, acc, bg + (2 * u + 1) * BT_TABLE + (dB < 0 ? -dB : dB) * BT_WORDS, dB < 0);
+        if (u < 3) ge_p1p1_to_p3(acc, t);
+        else ge_p1p1_to_p2(r2, t);
+        const uint32_t x = so[0];
+        so[0] = so[1]; so[1] = so[2]; so[2] = so[3]; so[3] = x;
       }
-      if (bwin) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int dB = (int)((sw[q] >> (8 * (i >> 1))) & 255u) - 128;
-          ge_madd_at(t, acc, btab4 + (q * BT_ENTRIES + (dB < 0 ? -dB : dB)) * BT_WORDS, dB < 0);
-          if (q < 3) ge_p1p1_to_p3(acc, t);
-        }
-      }
-      ge_p1p1_to_p2(r2, t);
     }
   }
   out = r2;
@@ -627,7 +653,7 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
 
 // R' = h(-A) + S B with -A's comb tables taken from a prepared key
 PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, const uint32_t* dig_src,
-                             const uint32_t* btab4) {
+                             const uint32_t* bl, const uint32_t* bg) {
   if (!kt[KEY_STATUS]) return false;
   uint32_t hh[8], S[8];
   {
@@ -637,7 +663,7 @@ PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, 
     sc_reduce64(hh, dig);
   }
   load8(S, sig + 32);
-  double_scalarmult_comb(rp, hh, S, kt, btab4);
+  double_scalarmult_comb(rp, hh, S, kt, bl, bg);
   return true;
 }
 
@@ -675,11 +701,12 @@ PV_HD void batch_invert_z(uint32_t* pts, int K) {
 // accepted bitmask.  Rejected or absent entries carry Z = 1 through the
 // shared inversion.  scratch = LANE_WORDS words owned by this lane.
 // KEYED: signature i uses prepared key kidx[i] (comb tables in ktab; btab
-// then holds the four quarter tables).
+// then holds the even chunk tables 0, 2, 4, 6 and bg all eight).
 template <bool KEYED>
 PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre, uint64_t i0,
                            uint64_t stride, uint64_t n, uint32_t* scratch, const uint32_t* btab,
-                           const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
+                           const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr,
+                           const uint32_t* bg = nullptr) {
   uint32_t* pts = scratch + AT_WORDS;
   uint32_t live = 0;
 #pragma unroll 1
@@ -689,7 +716,7 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     bool ok = false;
     if (i < n && pre[i]) {
       if constexpr (KEYED)
-        ok = curve_point_keyed(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, btab);
+        ok = curve_point_keyed(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, btab, bg);
       else
         ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);
     }

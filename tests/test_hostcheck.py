@@ -145,7 +145,7 @@ def _run_mode(hc, pk, sig, blob, off, force_full):
     v = np.zeros(n, np.uint8)
     nd = ctypes.c_uint64()
     b = orc.padded(blob)
-    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())  # base-point tables outside the counted region
+    hc.hc_btable((ctypes.c_uint32 * (8 * 129 * 32))())  # base-point tables outside the counted region
     hc.hc_reset_counts()
     hc.hc_verify_batch_mode(_p(np.ascontiguousarray(pk)), _p(np.ascontiguousarray(sig)), _p(b),
                             _p(np.ascontiguousarray(off)), ctypes.c_uint64(n), _p(v), int(force_full), ctypes.byref(nd))
@@ -179,7 +179,7 @@ def test_op_counts_pin_grouped_constants(hc):
     import bench
     n = 16
     pk, sig, blob, off = _signed_batch(n, 4)
-    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())
+    hc.hc_btable((ctypes.c_uint32 * (8 * 129 * 32))())
     hc.hc_reset_counts()
     v = np.zeros(n, np.uint8)
     b = orc.padded(blob)
@@ -323,7 +323,7 @@ def test_op_counts_pin_keyed_constants(hc):
     blob = np.frombuffer(os.urandom(256 * n), np.uint8)
     off = np.arange(n + 1, dtype=np.uint64) * 256
     pk, sig = orc.sign_batch(seeds, blob, off)
-    hc.hc_btable((ctypes.c_uint32 * (4 * 129 * 32))())
+    hc.hc_btable((ctypes.c_uint32 * (8 * 129 * 32))())
     v = np.zeros(n, np.uint8)
 
     def run(upk, kidx, s, b):

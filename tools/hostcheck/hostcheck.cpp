@@ -57,13 +57,15 @@ static void hc_check_sq(const uint32_t* f) {
 
 using namespace pv;
 
-static uint32_t g_btab[COMB_Q * BT_ENTRIES * BT_WORDS];
+static uint32_t g_btab[BT_CHUNKS * BT_TABLE];
+static uint32_t g_btab_even[4 * BT_TABLE];   // chunks 0, 2, 4, 6 (the keyed kernel's LDS image)
 static int g_btab_ready = 0;
 
 static void ensure_btab() {
   if (g_btab_ready) return;
-  for (int q = 0; q < COMB_Q; ++q)
+  for (int q = 0; q < BT_CHUNKS; ++q)
     for (int k = 0; k < BT_ENTRIES; ++k) btable_entry(g_btab + (q * BT_ENTRIES + k) * BT_WORDS, k, q);
+  for (int t = 0; t < 4; ++t) memcpy(g_btab_even + t * BT_TABLE, g_btab + 2 * t * BT_TABLE, 4 * BT_TABLE);
   g_btab_ready = 1;
 }
 
@@ -86,7 +88,7 @@ void hc_verify_batch_mode(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
     const uint32_t st = lattice_one(rec, pre, h, sig + 64 * i, force_full != 0);
     bool ok = false;
     if (st == HS_HALF) {
-      ok = curve_half(pk + 32 * i, sig + 64 * i, rec, lane, g_btab, g_btab + 2 * BT_ENTRIES * BT_WORDS);
+      ok = curve_half(pk + 32 * i, sig + 64 * i, rec, lane, g_btab, g_btab + 4 * BT_TABLE);
     } else if (st == HS_DEFER) {
       ok = verify_full_one(pk + 32 * i, sig + 64 * i, h, lane, g_btab);
       ++nd;
@@ -155,7 +157,7 @@ void hc_verify_keyed(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const 
   for (uint64_t i = 0; i < n; ++i)
     pre[i] = hash_one(h + 16 * i, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
   for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
-    const uint32_t okm = curve_group<true>(pk, sig, h, pre, i0, 1, n, lane, g_btab, ktab, kidx);
+    const uint32_t okm = curve_group<true>(pk, sig, h, pre, i0, 1, n, lane, g_btab_even, ktab, kidx, g_btab);
     for (int q = 0; q < CURVE_K && i0 + q < n; ++q) verdict[i0 + q] = (okm >> q) & 1u;
   }
   free(ktab);
