@@ -214,6 +214,12 @@ int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *
 int pv_set_curve_mode(uint32_t mode);
 int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 
+/* Live kernel timing of the verify calls themselves (bench.py's timed region):
+ * enable = 1 resets and starts recording HIP events around the hash and curve
+ * stages of every verify launch on `device` (on the launch stream); enable = 0
+ * stops and returns the summed milliseconds and the number of launches. */
+int pv_kernel_timing(int device, int enable, float *hash_ms, float *curve_ms, uint64_t *launches);
+
 /* pv_time_verify_device for keyed batches. */
 int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk, const uint8_t *sig,
                                 const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n, uint8_t *verdict,

@@ -99,6 +99,10 @@ struct Device {
   int curve_half_blocks = 0;
   CurveMode mode = CurveMode::Half;
   bool half_ran = false;               // qc[0] holds the last generic batch's deferred count
+  // pv_kernel_timing: HIP-event times of every verify launch while enabled
+  bool live_timing = false;
+  float live_hash = 0, live_curve = 0;
+  uint64_t live_launches = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -190,6 +194,13 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
                    uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed, float* ms_hash,
                    float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
   if (n == 0) return PV_OK;
+  const bool live = !timed && d.live_timing;
+  if (live) {
+    timed = true;
+    ms_hash = &d.live_hash;
+    ms_curve = &d.live_curve;
+    ++d.live_launches;
+  }
   HIP_OK(d.h.ensure(n * 16));
   HIP_OK(d.pre.ensure(n));
   uint64_t* bm = bitmap;
@@ -450,6 +461,21 @@ int pv_time_verify_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
   }
   if (ms_hash) *ms_hash = a / iters;
   if (ms_curve) *ms_curve = b / iters;
+  return PV_OK;
+}
+
+int pv_kernel_timing(int device, int enable, float* hash_ms, float* curve_ms, uint64_t* launches) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (enable) {
+    d->live_hash = d->live_curve = 0;
+    d->live_launches = 0;
+  }
+  if (hash_ms) *hash_ms = d->live_hash;
+  if (curve_ms) *curve_ms = d->live_curve;
+  if (launches) *launches = d->live_launches;
+  d->live_timing = enable != 0;
   return PV_OK;
 }
 

@@ -56,7 +56,19 @@ SIGNATURES = [
       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ('pv_curve_stats', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)]),
     ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
+    ('pv_kernel_timing', ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+      ctypes.POINTER(ctypes.c_uint64)]),
 ]
+
+
+def kernel_timing(device, enable):
+    """Start (enable=True) or stop live HIP-event timing of the verify launches on
+    `device` (pv_kernel_timing); stopping returns (hash_ms, curve_ms, launches) summed."""
+    h, c, k = ctypes.c_float(), ctypes.c_float(), ctypes.c_uint64()
+    _check('pv_kernel_timing', load().pv_kernel_timing(device, 1 if enable else 0, ctypes.byref(h), ctypes.byref(c),
+                                                       ctypes.byref(k)))
+    return h.value, c.value, k.value
 
 CURVE_MODES = {0: 'half', 1: 'full', 2: 'grouped'}   # PV_CURVE_HALF / _FULL / _GROUPED
 

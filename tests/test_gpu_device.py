@@ -106,6 +106,16 @@ def test_kernel_timer(torch_dev):
     b = SyntheticBatch(0, 65536, 256, cfg=2)
     th, tc = b.time_kernels(2)
     assert th > 0 and tc > 0 and tc > th
+    # live timing of ordinary verify calls (bench.py's timed region)
+    from plenum_gpu import _native as nat
+    nat.kernel_timing(0, True)
+    for _ in range(3):
+        b.verify()
+    h, c, k = nat.kernel_timing(0, False)
+    assert k == 3 and h > 0 and c > h
+    assert nat.kernel_timing(0, False)[2] == 3      # stopped: no more launches recorded
+    b.verify()
+    assert nat.kernel_timing(0, False)[2] == 3
 
 
 def _check_against_spec(b, mode, cfg, first, n, lo, hi, key_mod=0, n_nodes=25):
