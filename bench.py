@@ -189,6 +189,27 @@ def _sodium_did_verifier():
     return SodiumDidVerifier
 
 
+def end_to_end(batch, dedup, reps=3):
+    """Host-buffer rate of pv_verify_batch on this rank's workload: pk/sig/M in
+    pageable host memory -> H2D (chunked, overlapped with the kernels) -> hash +
+    curve -> D2H verdicts.  SURVEY.md 8(d)'s second number; never `value`."""
+    pk, sig = batch.pk.cpu().numpy(), batch.sig.cpu().numpy()
+    off = batch.off.cpu().numpy().astype(np.uint64)
+    blob = batch.blob.cpu().numpy()[:int(off[-1])]
+    want = ~batch.tamper.cpu().numpy().astype(bool)
+    got = nat.verify_batch_arrays(pk, sig, blob, off, device_mask=1 << batch.device.index, dedup_keys=dedup)
+    mism = int((got != want).sum())
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        nat.verify_batch_arrays(pk, sig, blob, off, device_mask=1 << batch.device.index, dedup_keys=dedup)
+    dt = (time.perf_counter() - t0) / reps
+    return {'value': round(batch.n / dt, 1), 'unit': 'verifies/s', 'ms': round(dt * 1e3, 3),
+            'verdict_mismatches': mism,
+            'path': 'pv_verify_batch from pageable host numpy buffers ({:.0f} MB in, {} B out): H2D chunks on a '
+                    'copy stream overlapped with hash + curve kernels, D2H verdicts; mean of {} calls'.format(
+                        (pk.nbytes + sig.nbytes + blob.nbytes + off.nbytes) / 1e6, batch.n, reps)}
+
+
 def main_c1(args):
     """C1: the Plenum request-authentication path end to end (host preprocessing
     + one GPU verify per batch) vs the same per-request path on libsodium."""
@@ -324,6 +345,7 @@ def main():
     ap.add_argument('--n', '--count', dest='n', type=int, default=None,
                     help='signatures per GPU (default: the config\'s); spell it --count under torch.distributed.run')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-e2e', action='store_true', help='skip the host-buffer (PCIe-inclusive) measurement')
     ap.add_argument('--no-key-cache', action='store_true',
                     help='c3/c4: re-decompress every key per signature instead of preparing each distinct key once')
     args = ap.parse_args()
@@ -493,6 +515,9 @@ def main():
         out['quorum_reached'] = int(tally['reached'].sum().item())
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(batch, args.config.upper())
+    if world == 1 and args.config == 'c2' and not args.no_e2e:
+        out['end_to_end'] = end_to_end(batch, key_cache)
+        mism += out['end_to_end']['verdict_mismatches']
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

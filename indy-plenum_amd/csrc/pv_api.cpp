@@ -7,6 +7,7 @@
 // message for pv_last_error().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -34,6 +35,11 @@ int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
+
+// host-buffer pipeline (pv_verify_batch): a shard runs as at most
+// PV_HOST_CHUNKS chunks of at least PV_HOST_CHUNK_MIN signatures
+#define PV_HOST_CHUNKS 8
+#define PV_HOST_CHUNK_MIN 65536
 
 #define HIP_OK(expr)                                                                          \
   do {                                                                                        \
@@ -74,6 +80,8 @@ enum class CurveMode { Half, Full, Grouped };
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
+  hipStream_t copy = nullptr;   // host-buffer calls: H2D of chunk c+1 overlaps the kernels of chunk c
+  hipEvent_t copied = nullptr;  // recorded on `copy` after each chunk's inputs, waited on by `stream`
   int cu_count = 0;
   int curve_blocks = 0;
   int hash_blocks = 0;
@@ -127,6 +135,8 @@ Device* find_dev(int id) {
 int init_device(Device& d) {
   HIP_OK(hipSetDevice(d.id));
   HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  HIP_OK(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d.id));
   d.cu_count = prop.multiProcessorCount;
@@ -184,6 +194,10 @@ void release_device(Device& d) {
   d.hrec.release(); d.dlist.release(); d.qc.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
+  if (d.copied) (void)hipEventDestroy(d.copied);
+  d.copied = nullptr;
+  if (d.copy) (void)hipStreamSynchronize(d.copy), (void)hipStreamDestroy(d.copy);
+  d.copy = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d.stream = nullptr;
   d.id = -1;
@@ -304,21 +318,47 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
   std::vector<Device*> devs = select_devs(device_mask);
   if (devs.empty()) return fail(PV_ENODEV, "device_mask 0x%x selects no initialised device", device_mask);
   const uint64_t G = devs.size();
-  std::vector<std::vector<uint64_t>> offs(G);
-  // enqueue every shard, then drain
+  // Per device: one shard [s, e).  Setup (offsets, key dedup, buffers, key
+  // preparation) first; then the shard runs as a pipeline of chunks: chunk c's
+  // inputs go H2D on the copy stream, the compute stream waits for them, runs
+  // hash + curve and copies the chunk's verdicts back.  The pageable H2D of
+  // chunk c + 1 (staged by the runtime on the host thread) then overlaps the
+  // kernels of chunk c.  Chunks index into the shard's buffers (offsets stay
+  // shard-relative), so no device buffer is reused while in flight.
+  struct Shard {
+    uint64_t s = 0, m = 0, chunk = 0;
+    std::vector<uint64_t> offs;
+    std::vector<uint8_t> upk;
+    std::vector<uint32_t> idx;
+    bool keyed = false;
+  };
+  std::vector<Shard> sh(G);
+  // on every exit (errors included) wait for the copies that read `sh` and the caller's buffers
+  struct Drain {
+    std::vector<Device*>& v;
+    ~Drain() {
+      for (Device* d : v) {
+        (void)hipSetDevice(d->id);
+        (void)hipStreamSynchronize(d->copy);
+        (void)hipStreamSynchronize(d->stream);
+      }
+    }
+  } drain{devs};
+  uint64_t max_chunks = 0;
   for (uint64_t g = 0; g < G; ++g) {
     Device& d = *devs[g];
+    Shard& z = sh[g];
     const uint64_t s = n * g / G, e = n * (g + 1) / G, m = e - s;
+    z.s = s;
+    z.m = m;
     if (m == 0) continue;
     HIP_OK(hipSetDevice(d.id));
     const uint64_t b0 = msg_off[s], bytes = msg_off[e] - b0;
-    offs[g].resize(m + 1);
-    for (uint64_t k = 0; k <= m; ++k) offs[g][k] = msg_off[s + k] - b0;
+    z.offs.resize(m + 1);
+    for (uint64_t k = 0; k <= m; ++k) z.offs[k] = msg_off[s + k] - b0;
     // PV_FLAG_DEDUP_KEYS: prepare each distinct key once (cached multiples of
     // -A) when at least half of the shard's signatures repeat a key
     uint64_t nk = m;
-    std::vector<uint8_t> upk;
-    std::vector<uint32_t> idx;
     if (flags & PV_FLAG_DEDUP_KEYS) {
       struct KeyHash {
         size_t operator()(const std::string& k) const {
@@ -329,47 +369,76 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
       };
       std::unordered_map<std::string, uint32_t, KeyHash> seen;
       seen.reserve(m);
-      idx.resize(m);
+      z.idx.resize(m);
       for (uint64_t k = 0; k < m; ++k) {
         auto it = seen.emplace(std::string(reinterpret_cast<const char*>(pk + 32 * (s + k)), 32), (uint32_t)seen.size());
-        if (it.second) upk.insert(upk.end(), pk + 32 * (s + k), pk + 32 * (s + k) + 32);
-        idx[k] = it.first->second;
+        if (it.second) z.upk.insert(z.upk.end(), pk + 32 * (s + k), pk + 32 * (s + k) + 32);
+        z.idx[k] = it.first->second;
       }
       nk = seen.size();
       if (2 * nk > m) {
         nk = m;
-        idx.clear();
+        z.idx.clear();
+        z.upk.clear();
       }
     }
-    const bool keyed = !idx.empty();
-    HIP_OK(d.pk.ensure((keyed ? nk : m) * 32));
+    z.keyed = !z.idx.empty();
+    HIP_OK(d.pk.ensure((z.keyed ? nk : m) * 32));
     HIP_OK(d.sig.ensure(m * 64));
     HIP_OK(d.blob.ensure(bytes + 16));
     HIP_OK(d.off.ensure(m + 1));
     HIP_OK(d.verdict.ensure(m));
-    if (keyed) {
+    // workspaces sized for the largest chunk before anything is in flight
+    z.chunk = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + PV_HOST_CHUNKS - 1) / PV_HOST_CHUNKS);
+    const uint64_t cm = std::min(m, z.chunk);
+    HIP_OK(d.h.ensure(cm * 16));
+    HIP_OK(d.pre.ensure(cm));
+    HIP_OK(d.bitmap.ensure((cm + 63) / 64));
+    HIP_OK(d.hrec.ensure(cm * pv::HSREC_WORDS));
+    HIP_OK(d.dlist.ensure(cm));
+    max_chunks = std::max(max_chunks, (m + z.chunk - 1) / z.chunk);
+    HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.copy));
+    if (z.keyed) {
       HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
       HIP_OK(d.kidx.ensure(m));
-      HIP_OK(hipMemcpyAsync(d.pk.p, upk.data(), nk * 32, hipMemcpyHostToDevice, d.stream));
-      HIP_OK(hipMemcpyAsync(d.kidx.p, idx.data(), m * 4, hipMemcpyHostToDevice, d.stream));
       HIP_OK(d.kscr.ensure(nk * pv::KEYTAB_SCRATCH));
+      HIP_OK(hipMemcpyAsync(d.pk.p, z.upk.data(), nk * 32, hipMemcpyHostToDevice, d.copy));
+      HIP_OK(hipMemcpyAsync(d.kidx.p, z.idx.data(), m * 4, hipMemcpyHostToDevice, d.copy));
+      HIP_OK(hipEventRecord(d.copied, d.copy));
+      HIP_OK(hipStreamWaitEvent(d.stream, d.copied, 0));
       HIP_OK(pv::launch_keys(d.pk.p, nk, d.ktab.p, d.kscr.p, d.stream));
-    } else {
-      HIP_OK(hipMemcpyAsync(d.pk.p, pk + 32 * s, m * 32, hipMemcpyHostToDevice, d.stream));
     }
-    HIP_OK(hipMemcpyAsync(d.sig.p, sig + 64 * s, m * 64, hipMemcpyHostToDevice, d.stream));
-    if (bytes) HIP_OK(hipMemcpyAsync(d.blob.p, msg_blob + b0, bytes, hipMemcpyHostToDevice, d.stream));
-    HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.stream));
-    HIP_OK(hipMemcpyAsync(d.off.p, offs[g].data(), (m + 1) * 8, hipMemcpyHostToDevice, d.stream));
-    int rc = enqueue_verify(d, d.pk.p, d.sig.p, d.blob.p, d.off.p, m, d.verdict.p, nullptr, d.stream, false, nullptr,
-                            nullptr, keyed ? d.ktab.p : nullptr, keyed ? d.kidx.p : nullptr);
-    if (rc) return rc;
-    // the key staging vectors die with this iteration: drain the shard's copies first
-    if (keyed) HIP_OK(hipStreamSynchronize(d.stream));
-    HIP_OK(hipMemcpyAsync(verdict + s, d.verdict.p, m, hipMemcpyDeviceToHost, d.stream));
   }
+  // chunk-major over devices, so every device's pipeline starts early
+  for (uint64_t c = 0; c < max_chunks; ++c) {
+    for (uint64_t g = 0; g < G; ++g) {
+      Device& d = *devs[g];
+      Shard& z = sh[g];
+      const uint64_t c0 = c * z.chunk;
+      if (c0 >= z.m) continue;
+      const uint64_t c1 = std::min(z.m, c0 + z.chunk), mc = c1 - c0;
+      HIP_OK(hipSetDevice(d.id));
+      const uint64_t b0 = msg_off[z.s], cb0 = z.offs[c0], cbytes = z.offs[c1] - cb0;
+      if (!z.keyed)
+        HIP_OK(hipMemcpyAsync(d.pk.p + 32 * c0, pk + 32 * (z.s + c0), mc * 32, hipMemcpyHostToDevice, d.copy));
+      HIP_OK(hipMemcpyAsync(d.sig.p + 64 * c0, sig + 64 * (z.s + c0), mc * 64, hipMemcpyHostToDevice, d.copy));
+      if (cbytes)
+        HIP_OK(hipMemcpyAsync(d.blob.p + cb0, msg_blob + b0 + cb0, cbytes, hipMemcpyHostToDevice, d.copy));
+      HIP_OK(hipMemcpyAsync(d.off.p + c0, z.offs.data() + c0, (mc + 1) * 8, hipMemcpyHostToDevice, d.copy));
+      HIP_OK(hipEventRecord(d.copied, d.copy));
+      HIP_OK(hipStreamWaitEvent(d.stream, d.copied, 0));
+      // blob base + shard-relative offsets: the hash kernel reads blob + off[i]
+      int rc = enqueue_verify(d, z.keyed ? d.pk.p : d.pk.p + 32 * c0, d.sig.p + 64 * c0, d.blob.p, d.off.p + c0, mc,
+                              d.verdict.p + c0, nullptr, d.stream, false, nullptr, nullptr,
+                              z.keyed ? d.ktab.p : nullptr, z.keyed ? d.kidx.p + c0 : nullptr);
+      if (rc) return rc;
+      HIP_OK(hipMemcpyAsync(verdict + z.s + c0, d.verdict.p + c0, mc, hipMemcpyDeviceToHost, d.stream));
+    }
+  }
+  // drain (the staging vectors in `sh` outlive every copy that reads them)
   for (uint64_t g = 0; g < G; ++g) {
     HIP_OK(hipSetDevice(devs[g]->id));
+    HIP_OK(hipStreamSynchronize(devs[g]->copy));
     HIP_OK(hipStreamSynchronize(devs[g]->stream));
   }
   return PV_OK;

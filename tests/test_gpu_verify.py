@@ -160,3 +160,28 @@ def test_keyed_device_path_c3_and_c4(nat):
         assert (bits == v1).all()
         th, tc = b.time_kernels(1)
         assert th > 0 and tc > 0
+
+
+@pytest.mark.parametrize('shape', ['c2', 'c4_keyed'])
+def test_host_pipeline_multi_chunk(nat, shape):
+    """pv_verify_batch runs a shard as a pipeline of chunks (H2D of chunk c+1 on
+    the copy stream overlaps the kernels of chunk c; >= 65536 signatures per
+    chunk): a 150k batch spans 3 chunks.  Verdicts == not tampered; the keyed
+    case (4096-key pool, ragged 128 B - 4 KB payloads) indexes the chunk's
+    key indices and shard-relative message offsets."""
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch
+    if shape == 'c2':
+        b = SyntheticBatch(0, 150000, 256, cfg=2, first=4242)
+    else:
+        b = SyntheticBatch(0, 150000, 128, cfg=4, first=999, key_mod=4096, mode=synth.RANGE, mlen_max=4096)
+    pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()
+    off = b.off.cpu().numpy().astype(np.uint64)
+    blob = b.blob.cpu().numpy()[:int(off[-1])]
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    for dedup in (False, True):
+        got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=dedup)
+        assert (got == want).all(), (shape, dedup, int((got != want).sum()))
+    # two full chunks and a 3-signature tail chunk
+    got = nat.verify_batch_arrays(pk[:131075], sig[:131075], blob[:int(off[131075])], off[:131076])
+    assert (got == want[:131075]).all()
