@@ -18,6 +18,9 @@ namespace pv {
 
 constexpr int BT_ENTRIES = 129;   // niels k*B, k = 0..128
 constexpr int BT_WORDS = 32;      // 3 fe (30 words) padded to 32
+#ifndef PV_HALF_PREFETCH
+#define PV_HALF_PREFETCH 1
+#endif
 constexpr int AT_ENTRY = 40;      // cached entry words
 constexpr int AT_WORDS = 9 * 40;  // k*(-A), k = 0..8
 
@@ -352,6 +355,37 @@ PV_HD void ge_madd_at(ge_p1p1& r, const ge_p3& p, const uint32_t* q, bool neg) {
   fe_sub(u, p.Y, p.X);
   load_fe(g, q + (neg ? 0 : 10));
   fe_mul(b, u, g);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_neg(u, c);
+  fe_cmov(c, c, u, neg);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);
+}
+
+// Register-operand form of ge_add_cached_at for software-pipelined table
+// reads: the entry is fetched (already sign-swapped) into registers well
+// before the add that consumes it, so its global-memory latency runs under
+// the doublings / the previous add instead of stalling the wave.
+struct ge_entry { fe a, b, z2, t2d; };
+
+template <int S = 1>
+PV_HD void load_entry(ge_entry& e, const uint32_t* q, bool neg) {
+  load_fe<S>(e.a, q + (neg ? 10 * S : 0));   // Y2+X2 (Y2-X2 for -Q)
+  load_fe<S>(e.b, q + (neg ? 0 : 10 * S));
+  load_fe<S>(e.z2, q + 20 * S);
+  load_fe<S>(e.t2d, q + 30 * S);
+}
+
+// same operation sequence (and operand bounds) as ge_add_cached_at
+PV_HD void ge_add_entry(ge_p1p1& r, const ge_p3& p, const ge_entry& e, bool neg) {
+  fe c, d, a, b, u;
+  fe_mul(c, e.t2d, p.T);
+  fe_mul(d, p.Z, e.z2);
+  fe_add(u, p.Y, p.X);
+  fe_mul(a, u, e.a);
+  fe_sub(u, p.Y, p.X);
+  fe_mul(b, u, e.b);
   fe_sub(r.X, a, b);
   fe_add(r.Y, a, b);
   fe_neg(u, c);
@@ -827,6 +861,13 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
     ge_p1p1_to_p2(r2, t);
   }
   uint32_t cw = cp[3], dw = dp[3], lw = sl[3], hw = sh[3];
+#if PV_HALF_PREFETCH
+  // software pipeline: the +-A entry of window w is loaded before its four
+  // doublings, the -R entry before the +-A add
+  ge_entry ea, er;
+  int dA = (int)((cw >> 28) & 15u) - 8;
+  load_entry<LS>(ea, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
+#endif
 #pragma unroll 1
   for (int w = 31; w >= 0; --w) {
     if ((w & 7) == 7 && w != 31) {
@@ -851,11 +892,19 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
     ge_p2_dbl(t, r2);
     ge_p1p1_to_p3(acc, t);
     const int sh4 = 4 * (w & 7);
+#if PV_HALF_PREFETCH
+    const int dR = (int)((dw >> sh4) & 15u) - 8;
+    load_entry<LS>(er, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY * LS, dR < 0);
+    ge_add_entry(t, acc, ea, dA < 0);
+    ge_p1p1_to_p3(acc, t);
+    ge_add_entry(t, acc, er, dR < 0);
+#else
     const int dA = (int)((cw >> sh4) & 15u) - 8;
     ge_add_cached_at<LS>(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
     ge_p1p1_to_p3(acc, t);
     const int dR = (int)((dw >> sh4) & 15u) - 8;
     ge_add_cached_at<LS>(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY * LS, dR < 0);
+#endif
     if ((w & 1) == 0) {
       const int sh8 = 8 * ((w >> 1) & 3);
       const int dL = (int)((lw >> sh8) & 255u) - 128;
@@ -866,6 +915,14 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
       ge_madd_at(t, acc, bhi + (dH < 0 ? -dH : dH) * BT_WORDS, dH < 0);
     }
     if (w == 0) break;
+#if PV_HALF_PREFETCH
+    {
+      // digit of window w - 1: its word is cp[2] when w - 1 starts a new word
+      const uint32_t nw = ((w - 1) & 7) == 7 ? cp[2] : cw;
+      dA = (int)((nw >> (4 * ((w - 1) & 7))) & 15u) - 8;
+      load_entry<LS>(ea, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
+    }
+#endif
     ge_p1p1_to_p2(r2, t);
   }
 }
