@@ -18,6 +18,9 @@ namespace pv {
 
 constexpr int BT_ENTRIES = 129;   // niels k*B, k = 0..128
 constexpr int BT_WORDS = 32;      // 3 fe (30 words) padded to 32
+#ifndef PV_COMB_PREFETCH
+#define PV_COMB_PREFETCH 1
+#endif
 #ifndef PV_HALF_PREFETCH
 #define PV_HALF_PREFETCH 1
 #endif
@@ -394,6 +397,33 @@ PV_HD void ge_add_entry(ge_p1p1& r, const ge_p3& p, const ge_entry& e, bool neg)
   fe_sub(r.T, d, c);
 }
 
+// affine (niels) entry in registers, sign-swapped at load: same operation
+// sequence and bounds as ge_madd_at
+struct ge_nentry { fe a, b, c; };
+
+PV_HD void load_nentry(ge_nentry& e, const uint32_t* q, bool neg) {
+  load_fe(e.a, q + (neg ? 10 : 0));   // y2+x2 (y2-x2 for -Q)
+  load_fe(e.b, q + (neg ? 0 : 10));
+  load_fe(e.c, q + 20);               // 2d*x2*y2
+}
+
+PV_HD void ge_madd_entry(ge_p1p1& r, const ge_p3& p, const ge_nentry& e, bool neg) {
+  fe c, d, a, b, u;
+  fe_mul(c, e.c, p.T);
+  fe_add(d, p.Z, p.Z);
+  fe_carry(d);
+  fe_add(u, p.Y, p.X);
+  fe_mul(a, u, e.a);
+  fe_sub(u, p.Y, p.X);
+  fe_mul(b, u, e.b);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_neg(u, c);
+  fe_cmov(c, c, u, neg);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);
+}
+
 // ----------------------------------------------------------------- curve
 // cached multiples 0..8 of P into a per-lane table (9 x 40 words)
 template <int LS = 1>
@@ -637,6 +667,11 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
   ge_p3_0(acc);
   ge_p1p1 t;
   ge_p2 r2;
+#if PV_COMB_PREFETCH
+  ge_nentry ea, eb;
+  int dA = (int)((hp[0] >> 28) & 15u) - 8;
+  load_nentry(ea, kt + (dA < 0 ? -dA : dA) * KT_ENTRY, dA < 0);
+#endif
 #pragma unroll 1
   for (int w = 7; w >= 0; --w) {
     if (w != 7) {
@@ -650,6 +685,39 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
     }
     const int sh4 = 4 * w;
     const bool bwin = (w & 1) == 0;
+#if PV_COMB_PREFETCH
+    // two key adds per trip, ping-ponging the register entries: the entry of
+    // the next add (hp[1] holds its digit word; q = 0 of window w - 1 after
+    // the last one) is in flight during the current add
+#pragma unroll 1
+    for (int q = 0; q < COMB_Q; q += 2) {
+      {
+        const int dn = (int)((hp[1] >> sh4) & 15u) - 8;
+        load_nentry(eb, kt + (q + 1) * KT_TABLE + (dn < 0 ? -dn : dn) * KT_ENTRY, dn < 0);
+        ge_madd_entry(t, acc, ea, dA < 0);
+        ge_p1p1_to_p3(acc, t);
+        const uint32_t x = hp[0];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) hp[j] = hp[j + 1];
+        hp[7] = x;
+        dA = dn;
+      }
+      {
+        const bool last = q + 2 >= COMB_Q;
+        const bool more = !last || w > 0;
+        const int dn = (int)((hp[1] >> ((last ? sh4 - 4 : sh4) & 31)) & 15u) - 8;
+        if (more) load_nentry(ea, kt + (last ? 0 : q + 2) * KT_TABLE + (dn < 0 ? -dn : dn) * KT_ENTRY, dn < 0);
+        ge_madd_entry(t, acc, eb, dA < 0);
+        if (!last || bwin) ge_p1p1_to_p3(acc, t);
+        else ge_p1p1_to_p2(r2, t);          // a doubling comes next: no T needed
+        const uint32_t x = hp[0];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) hp[j] = hp[j + 1];
+        hp[7] = x;
+        dA = dn;
+      }
+    }
+#else
 #pragma unroll 1
     for (int q = 0; q < COMB_Q; ++q) {
       const int dA = (int)((hp[0] >> sh4) & 15u) - 8;
@@ -661,6 +729,7 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
       for (int j = 0; j < 7; ++j) hp[j] = hp[j + 1];
       hp[7] = x;
     }
+#endif
     if (bwin) {
       const int sh8 = 8 * (w >> 1);
 #pragma unroll 1

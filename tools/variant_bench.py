@@ -32,6 +32,7 @@ def main():
     ap.add_argument('--mlen-max', type=int, default=None)
     ap.add_argument('--key-mod', type=int, default=0)
     ap.add_argument('--cfg', type=int, default=2)
+    ap.add_argument('--keyed', action='store_true', help='prepared-key path (key pool --key-mod or COMMIT node keys)')
     ap.add_argument('--no-check', action='store_true', help='timing experiments whose verdicts are knowingly wrong')
     a = ap.parse_args()
     b = SyntheticBatch(0, a.n, a.mlen, cfg=a.cfg, mode=a.mode, mlen_max=a.mlen_max, key_mod=a.key_mod)
@@ -48,13 +49,24 @@ def main():
         assert lib.pv_init(1) == 0, lib.pv_last_error()
         libs.append((os.path.basename(path), lib))
     res = {n: [] for n, _ in libs}
+    keys = b.key_index() if a.keyed else None
+    if a.keyed:
+        assert keys is not None, 'keyed timing needs --key-mod or --mode 2'
+        ktab = torch.empty(keys[0].shape[0] * nat.PV_KEY_WORDS, dtype=torch.int32, device=b.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for r in range(a.rounds):
         for name, lib in libs:
             h, c = ctypes.c_float(), ctypes.c_float()
             b.verdict.zero_()
-            rc = lib.pv_time_verify_device(_p(b.pk), _p(b.sig), _p(b.blob), _p(b.off), a.n, _p(b.verdict),
-                                           _p(b.bitmap), 0, stream, 2, ctypes.byref(h), ctypes.byref(c))
+            if keys is not None:
+                upk, kidx = keys
+                assert lib.pv_keys_prepare_device(_p(upk), upk.shape[0], _p(ktab), 0, stream) == 0, lib.pv_last_error()
+                rc = lib.pv_time_verify_keyed_device(_p(ktab), _p(kidx), _p(upk), _p(b.sig), _p(b.blob), _p(b.off),
+                                                     a.n, _p(b.verdict), _p(b.bitmap), 0, stream, 2,
+                                                     ctypes.byref(h), ctypes.byref(c))
+            else:
+                rc = lib.pv_time_verify_device(_p(b.pk), _p(b.sig), _p(b.blob), _p(b.off), a.n, _p(b.verdict),
+                                               _p(b.bitmap), 0, stream, 2, ctypes.byref(h), ctypes.byref(c))
             assert rc == 0, lib.pv_last_error()
             v = b.verdict.cpu().numpy().astype(bool)
             assert a.no_check or (v == ~tamper).all(), name
