@@ -566,6 +566,7 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
   kt[KEY_STATUS] = ok ? 1u : 0u;
   if (!ok) return;
   // projective multiples k * A_q (X, Y, Z) into the entry slots
+  fe zacc;
 #pragma unroll 1
   for (int q = 0; q < COMB_Q; ++q) {
     uint32_t* tq = kt + q * KT_TABLE;
@@ -573,12 +574,19 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
     ge_p3_to_cached(c1, P);
     ge_p3 Q = P;
     store_xyz(tq + KT_ENTRY, Q);
+    // prefix products of the Z's for the shared inversion, formed while each
+    // Z is in registers (entry e = 8 q + k - 1)
+    if (q == 0) fe_copy(zacc, Q.Z);
+    else fe_mul(zacc, zacc, Q.Z);
+    store_fe(scr + 10 * (8 * q), zacc);
 #pragma unroll 1
     for (int k = 2; k <= 8; ++k) {
       ge_p1p1 t;
       ge_add_cached(t, Q, c1, false);
       ge_p1p1_to_p3(Q, t);
       store_xyz(tq + k * KT_ENTRY, Q);
+      fe_mul(zacc, zacc, Q.Z);
+      store_fe(scr + 10 * (8 * q + k - 1), zacc);
     }
     if (q + 1 < COMB_Q) {  // A_{q+1} = 2^32 A_q = 2^29 (8 A_q)
       ge_p1p1 t;
@@ -595,35 +603,43 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
       ge_p1p1_to_p3(P, t);
     }
   }
-  // one inversion for all 8 * COMB_Q Z's (Montgomery's trick; prefix products in scr)
+  // one inversion for all 8 * COMB_Q Z's (Montgomery's trick; prefix
+  // products in scr).  Backward pass with the next entry's operands (X, Y, Z
+  // of entry e - 1, prefix e - 2) fetched one iteration ahead.
   constexpr int NE = 8 * COMB_Q;
-  fe acc, z, u;
-#pragma unroll 1
-  for (int e = 0; e < NE; ++e) {
-    const uint32_t* slot = kt + (e >> 3) * KT_TABLE + ((e & 7) + 1) * KT_ENTRY;
-    load_fe(z, slot + 20);
-    if (e == 0) fe_copy(acc, z);
-    else fe_mul(acc, acc, z);
-    store_fe(scr + 10 * e, acc);
-  }
-  fe_invert(acc, acc);
+  fe acc, u, z, x, y, un, zn, xn, yn;
+  fe_invert(acc, zacc);
   fe d2;
   fe_const_d2(d2);
+  {
+    const uint32_t* slot = kt + ((NE - 1) >> 3) * KT_TABLE + (((NE - 1) & 7) + 1) * KT_ENTRY;
+    load_fe(un, scr + 10 * (NE - 2));
+    load_fe(zn, slot + 20);
+    load_fe(xn, slot);
+    load_fe(yn, slot + 10);
+  }
 #pragma unroll 1
   for (int e = NE - 1; e >= 0; --e) {
     uint32_t* slot = kt + (e >> 3) * KT_TABLE + ((e & 7) + 1) * KT_ENTRY;
-    fe zi, x, y;
+    fe_copy(u, un);
+    fe_copy(z, zn);
+    fe_copy(x, xn);
+    fe_copy(y, yn);
     if (e > 0) {
-      load_fe(u, scr + 10 * (e - 1));
+      const uint32_t* nslot = kt + ((e - 1) >> 3) * KT_TABLE + (((e - 1) & 7) + 1) * KT_ENTRY;
+      if (e > 1) load_fe(un, scr + 10 * (e - 2));
+      load_fe(zn, nslot + 20);
+      load_fe(xn, nslot);
+      load_fe(yn, nslot + 10);
+    }
+    fe zi;
+    if (e > 0) {
       fe_mul(zi, acc, u);            // Z_e^-1
-      load_fe(z, slot + 20);
       fe_mul(acc, acc, z);           // (Z_0 ... Z_{e-1})^-1
     } else {
       fe_copy(zi, acc);
     }
-    load_fe(x, slot);
     fe_mul(x, x, zi);
-    load_fe(y, slot + 10);
     fe_mul(y, y, zi);
     fe_add(u, y, x); fe_carry(u);
     store_fe(slot, u);

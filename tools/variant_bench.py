@@ -50,6 +50,7 @@ def main():
         libs.append((os.path.basename(path), lib))
     res = {n: [] for n, _ in libs}
     keys = b.key_index() if a.keyed else None
+    kms = {}
     if a.keyed:
         assert keys is not None, 'keyed timing needs --key-mod or --mode 2'
         ktab = torch.empty(keys[0].shape[0] * nat.PV_KEY_WORDS, dtype=torch.int32, device=b.device)
@@ -60,7 +61,12 @@ def main():
             b.verdict.zero_()
             if keys is not None:
                 upk, kidx = keys
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
                 assert lib.pv_keys_prepare_device(_p(upk), upk.shape[0], _p(ktab), 0, stream) == 0, lib.pv_last_error()
+                e1.record()
+                e1.synchronize()
+                kms.setdefault(name, []).append(e0.elapsed_time(e1))
                 rc = lib.pv_time_verify_keyed_device(_p(ktab), _p(kidx), _p(upk), _p(b.sig), _p(b.blob), _p(b.off),
                                                      a.n, _p(b.verdict), _p(b.bitmap), 0, stream, 2,
                                                      ctypes.byref(h), ctypes.byref(c))
@@ -77,6 +83,10 @@ def main():
         hs = sorted(v[0] for v in vals)
         out[name] = {'curve_ms_median': cs[len(cs) // 2], 'curve_ms_min': cs[0], 'hash_ms_median': hs[len(hs) // 2],
                      'verifies_per_s_kernel': a.n / ((cs[len(cs) // 2] + hs[len(hs) // 2]) * 1e-3)}
+        if name in kms:
+            ks = sorted(kms[name])
+            out[name]['keys_ms_median'] = ks[len(ks) // 2]
+            out[name]['distinct_keys'] = int(keys[0].shape[0])
     print(json.dumps(out, indent=1))
 
 
