@@ -167,18 +167,31 @@ PV_HD void msg_fetch(uint32_t y[MSG_Y], const uint8_t* m, uint64_t mlen, uint64_
 
 // 32 little-endian words = message bytes [q, q + 128) with SHA padding applied:
 // bytes past mlen are zero and byte mlen is 0x80 (funnel shift of the raw words)
+// (a & m) | (b & ~m) as one v_bitop3_b32 (an intrinsic the compiler cannot
+// turn back into a select of addresses)
+PV_HD uint32_t bitsel(uint32_t m, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xca);
+#else
+  return (a & m) | (b & ~m);
+#endif
+}
+
 PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[MSG_Y], const uint8_t* m, uint64_t mlen, uint64_t q) {
-  const int64_t rem = (int64_t)mlen - (int64_t)q;
+  const int64_t rem64 = (int64_t)mlen - (int64_t)q;
+  // rem clamped to [-1, 132] (every word full above 128, all zero below 0)
+  const int32_t rem = rem64 < 0 ? -1 : (rem64 > 132 ? 132 : (int32_t)rem64);
   const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + q) & 3u);
+  // the one word holding byte `rem` keeps its low rem % 4 bytes and takes the
+  // 0x80 pad byte; masks are the same for every k, so each word costs one
+  // and-or and two compare-selects (branch-free: no divergent stores)
+  const uint32_t rb = 8u * ((uint32_t)rem & 3u);
+  const uint32_t keep = (1u << rb) - 1u, pad = 0x80u << rb;
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    uint32_t v = funnel32(y[k + 1], y[k], 8u * mis);
-    const int64_t r = rem - 4 * k;
-    if (r < 4) {
-      const uint32_t keep = r <= 0 ? 0u : (1u << (8 * (uint32_t)r)) - 1u;
-      v = (v & keep) | ((r >= 0) ? (0x80u << (8 * (uint32_t)r)) : 0u);
-    }
-    x[k] = v;
+    const uint32_t v = funnel32(y[k + 1], y[k], 8u * mis);
+    const uint32_t t = (v & keep) | pad;
+    x[k] = rem >= 4 * k + 4 ? v : (rem >= 4 * k ? t : 0u);
   }
 }
 
@@ -186,26 +199,28 @@ PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[MSG_Y], const uint8_t* 
 // words of hram_q(blk) (R, A read from sig/pk on block 0; length words on the last)
 PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[MSG_Y], const uint8_t* sig, const uint8_t* pk,
                          const uint8_t* m, uint64_t mlen, uint64_t blk, uint64_t nblk) {
-  const bool first = blk == 0;
+  const bool first = blk == 0, last = blk + 1 == nblk;
   uint32_t x[32];
   msg_assemble(x, y, m, mlen, hram_q(blk));
+  uint32_t ra[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) ra[j] = 0;
   if (first) {
-    uint32_t ra[16];
     load8(ra, sig);
     load8(ra + 8, pk);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      w[j] = be64_from_le32(ra[2 * j], ra[2 * j + 1]);
-      w[8 + j] = be64_from_le32(x[2 * j], x[2 * j + 1]);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = be64_from_le32(x[2 * j], x[2 * j + 1]);
   }
-  if (blk + 1 == nblk) {
-    w[14] = 0;
-    w[15] = (64 + mlen) * 8;
+  // per-word bitwise selects at static indices: a `?:` between two elements
+  // of x is folded by the compiler into ONE load at a computed index, which
+  // forces x into private memory (scratch) -- the opaque bit-select keeps the
+  // block in registers
+  const uint32_t fm = first ? 0xffffffffu : 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    w[j] = be64_from_le32(bitsel(fm, ra[2 * j], x[2 * j]), bitsel(fm, ra[2 * j + 1], x[2 * j + 1]));
+    w[8 + j] = be64_from_le32(bitsel(fm, x[2 * j], x[16 + 2 * j]), bitsel(fm, x[2 * j + 1], x[16 + 2 * j + 1]));
   }
+  w[14] = last ? 0 : w[14];
+  w[15] = last ? (64 + mlen) * 8 : w[15];
 }
 
 PV_HD void hram_block(uint64_t w[16], const uint8_t* sig, const uint8_t* pk, const uint8_t* m, uint64_t mlen,
