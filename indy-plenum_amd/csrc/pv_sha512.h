@@ -9,6 +9,10 @@
 #include <stdint.h>
 #include "pv_field.h"
 
+#ifndef PV_SHA_ASM_ADD
+#define PV_SHA_ASM_ADD 1
+#endif
+
 namespace pv {
 
 // first 64 bits of the fractional parts of the cube roots of the first 80
@@ -115,16 +119,30 @@ PV_HD uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) { return (e & f) | (~e &
 PV_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return (a & b) | (a & c) | (b & c); }
 #endif
 
+// 64-bit add as ONE v_lshl_add_u64 on the two register pairs.  Plain `+` on
+// values assembled from 32-bit halves (rotates, bit functions) is split by
+// the compiler into a zero-extended low add plus a 32-bit high add and moves
+// of a zero register (3 extra instructions per round).
+PV_HD uint64_t add64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && PV_SHA_ASM_ADD
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return a + b;
+#endif
+}
+
 // one compression; w[16] holds the block as big-endian-decoded 64-bit words
 // (it is overwritten by the schedule).  Per round: 6 alignbit + 2 bitop3 per
 // Sigma, 2 bitop3 for Ch, 2 for Maj, 7 64-bit adds.
 PV_HD void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t& e, uint64_t& f, uint64_t& g,
                         uint64_t& k, uint64_t kw) {
   const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
-  const uint64_t t1 = k + S1 + ch64(e, f, g) + kw;
+  const uint64_t t1 = add64(add64(add64(k, kw), ch64(e, f, g)), S1);
   const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
-  const uint64_t t2 = S0 + maj64(a, b, c);
-  k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  const uint64_t t2 = add64(S0, maj64(a, b, c));
+  k = g; g = f; f = e; e = add64(d, t1); d = c; c = b; b = a; a = add64(t1, t2);
 }
 
 PV_HD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
@@ -141,7 +159,7 @@ PV_HD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
       const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
       const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
       const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
-      w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+      w[j] = add64(add64(add64(w[j], w[(j + 9) & 15]), s0), s1);
       sha512_round(a, b, c, d, e, f, g, k, PV_SHA512_K[r + j] + w[j]);
     }
   }
