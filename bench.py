@@ -61,7 +61,9 @@ CONFIGS = {
 # half of all points: the mean is a whole number of multiplies), two 9-entry
 # tables, 33 windows, identity test instead of an inversion.  Deferred records
 # (~0.2 %) take the full-length verdict (W_*_FULL: 253 doublings + inversion).
-W_MUL_PER_VERIFY = 1299.0
+# s' B uses signed radix-2^16 digits (8 pairs of affine adds from the tables of
+# B and 2^128 B; radix 256 needed 16 pairs: 1299 multiplies per verify).
+W_MUL_PER_VERIFY = 1187.0
 W_SQ_PER_VERIFY = 1022.0
 W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
 W_MUL_FULL, W_SQ_FULL = 1587.5, 1517.0

@@ -86,6 +86,7 @@ struct Device {
   int curve_blocks = 0;
   int hash_blocks = 0;
   DevBuf<uint32_t> btab;
+  DevBuf<uint32_t> bw;        // radix-2^16 base-point tables of the half-size path
   DevBuf<uint32_t> scratch;   // per-lane A tables for the persistent curve grid
   DevBuf<uint32_t> h;         // SHA-512 digest, 16 words per signature
   DevBuf<unsigned long long> counter;  // hash-kernel work queue
@@ -142,6 +143,8 @@ int init_device(Device& d) {
   d.cu_count = prop.multiProcessorCount;
   HIP_OK(d.btab.ensure(pv::BTAB_CHUNKS * pv::BTAB_ENTRIES * pv::BTAB_WORDS));
   HIP_OK(pv::launch_btable_init(d.btab.p, d.stream));
+  HIP_OK(d.bw.ensure(pv::BWTAB_WORDS));
+  HIP_OK(pv::launch_bw_init(d.bw.p, d.stream));
   // persistent curve grid: resident blocks per CU from the occupancy query
   // (kept <= 4 blocks of 256 threads per CU, see cdna_hip_programming.md §1)
   int per_cu = 0;
@@ -186,7 +189,7 @@ void release_device(Device& d) {
   if (d.id < 0) return;
   (void)hipSetDevice(d.id);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
-  d.btab.release(); d.scratch.release(); d.h.release(); d.pre.release(); d.counter.release();
+  d.btab.release(); d.bw.release(); d.scratch.release(); d.h.release(); d.pre.release(); d.counter.release();
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.bitmap.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
@@ -236,7 +239,7 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
                               d.mode == CurveMode::Full, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (half) {
-    HIP_OK(pv::launch_curve_half(pk, sig, d.h.p, d.hrec.p, d.btab.p, d.scratch.p,
+    HIP_OK(pv::launch_curve_half(pk, sig, d.h.p, d.hrec.p, d.btab.p, d.bw.p, d.scratch.p,
                                  d.scratch.cap / pv::HALF_SCRATCH_WORDS, verdict, bm, n, d.dlist.p, d.qc.p, d.qc.p + 1,
                                  d.curve_half_blocks, s));
     d.half_ran = true;

@@ -58,10 +58,15 @@ hipError_t curve_half_occupancy(int* blocks_per_cu);
 hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t* pre, uint64_t n, uint32_t* rec,
                           uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks, uint64_t* bitmap,
                           bool force_full, hipStream_t s);
+// btab: the radix-256 base-point tables (deferred full-length tasks); bw:
+// BWTAB_WORDS words, the radix-2^16 tables of B and 2^128 B (launch_bw_init)
+constexpr int BWTAB_ENTRIES = (1 << 15) + 1;
+constexpr uint64_t BWTAB_WORDS = 2ull * BWTAB_ENTRIES * BTAB_WORDS;
+hipError_t launch_bw_init(uint32_t* bw, hipStream_t s);
 hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, const uint32_t* rec,
-                             const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
-                             uint64_t* bitmap, uint64_t n, const uint32_t* dlist, const unsigned long long* dcount,
-                             unsigned long long* tasks, int blocks, hipStream_t s);
+                             const uint32_t* btab, const uint32_t* bw, uint32_t* scratch, uint64_t scratch_lanes,
+                             uint8_t* verdict, uint64_t* bitmap, uint64_t n, const uint32_t* dlist,
+                             const unsigned long long* dcount, unsigned long long* tasks, int blocks, hipStream_t s);
 
 // prepared keys: KEYTAB_WORDS words per key (8 comb tables of affine multiples
 // k * 2^(32 q) * (-A) + status); KEYTAB_SCRATCH words of scratch per key

@@ -34,7 +34,8 @@ namespace pv {
 
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
                   KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && BT_CHUNKS == BTAB_CHUNKS &&
-                  HREC_WORDS == HSREC_WORDS && HALF_LANE_WORDS == HALF_SCRATCH_WORDS,
+                  HREC_WORDS == HSREC_WORDS && HALF_LANE_WORDS == HALF_SCRATCH_WORDS &&
+                  BW_ENTRIES == BWTAB_ENTRIES,
               "table layout");
 
 // ------------------------------------------------------------- hash kernel
@@ -232,17 +233,13 @@ __global__ __launch_bounds__(256) void k_lattice(const uint8_t* __restrict__ sig
 // LDS: tables of B and 2^128 B (2 x 16.5 KB).
 __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
     const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint32_t* __restrict__ dig,
-    const uint32_t* __restrict__ rec, const uint32_t* __restrict__ btab_g, uint32_t* __restrict__ scratch,
-    uint8_t* __restrict__ verdict, unsigned long long* __restrict__ bitmap, uint64_t n,
-    const uint32_t* __restrict__ dlist, const unsigned long long* __restrict__ dcount,
+    const uint32_t* __restrict__ rec, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ bw,
+    uint32_t* __restrict__ scratch, uint8_t* __restrict__ verdict, unsigned long long* __restrict__ bitmap,
+    uint64_t n, const uint32_t* __restrict__ dlist, const unsigned long long* __restrict__ dcount,
     unsigned long long* __restrict__ tasks) {
-  constexpr int TW = BTAB_ENTRIES * BTAB_WORDS;
-  __shared__ uint32_t btab[2 * TW];
-  for (int j = threadIdx.x; j < TW; j += CURVE_BLOCK) {
-    btab[j] = btab_g[j];                 // q = 0: B
-    btab[TW + j] = btab_g[4 * TW + j];   // q = 4: 2^128 B
-  }
-  __syncthreads();
+  // base-point tables stay in global memory (L2/MALL): btab (radix 256, q = 0)
+  // for the deferred full-length tasks, bw (radix 2^16, B and 2^128 B) for the
+  // half-size verdicts; their entries are fetched ahead of use
   const int lane = (int)(threadIdx.x & 63u);
   // per-lane tables interleaved by PV_HALF_LS lanes ([word][lane] inside each
   // group of PV_HALF_LS consecutive lanes): coalesced table loads
@@ -269,7 +266,7 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
       uint32_t st = HS_NONE;
       if (i < n) st = rec[HREC_WORDS * i + HREC_FLAGS] & 0xffu;
       bool ok = false;
-      if (st == HS_HALF) ok = curve_half<PV_HALF_LS>(pk + 32 * i, sig + 64 * i, rec + HREC_WORDS * i, scr, btab, btab + TW);
+      if (st == HS_HALF) ok = curve_half<PV_HALF_LS>(pk + 32 * i, sig + 64 * i, rec + HREC_WORDS * i, scr, bw, bw + BW_TABLE);
       const uint64_t ball = __ballot(ok);
       if (i < n && st != HS_DEFER) verdict[i] = ok ? 1 : 0;
       if (lane == 0 && ball) atomicOr(&bitmap[t - full_tasks], (unsigned long long)ball);
@@ -298,16 +295,26 @@ hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(64) void k_bw_init(uint32_t* bw) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < 2 * BW_ENTRIES) btable_entry(bw + (uint64_t)g * BT_WORDS, g % BW_ENTRIES, g < BW_ENTRIES ? 0 : 4, 16);
+}
+
+hipError_t launch_bw_init(uint32_t* bw, hipStream_t s) {
+  hipLaunchKernelGGL(k_bw_init, dim3((2 * BW_ENTRIES + 63) / 64), dim3(64), 0, s, bw);
+  return hipGetLastError();
+}
+
 hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, const uint32_t* rec,
-                             const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
-                             uint64_t* bitmap, uint64_t n, const uint32_t* dlist, const unsigned long long* dcount,
-                             unsigned long long* tasks, int blocks, hipStream_t s) {
+                             const uint32_t* btab, const uint32_t* bw, uint32_t* scratch, uint64_t scratch_lanes,
+                             uint8_t* verdict, uint64_t* bitmap, uint64_t n, const uint32_t* dlist,
+                             const unsigned long long* dcount, unsigned long long* tasks, int blocks, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t need = (n + CURVE_BLOCK - 1) / CURVE_BLOCK;
   uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
   if (b * CURVE_BLOCK > scratch_lanes) b = scratch_lanes / CURVE_BLOCK;
   if (b == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_curve_half, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, dig, rec, btab, scratch,
+  hipLaunchKernelGGL(k_curve_half, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, dig, rec, btab, bw, scratch,
                      verdict, reinterpret_cast<unsigned long long*>(bitmap), n, dlist, dcount, tasks);
   return hipGetLastError();
 }

@@ -297,7 +297,7 @@ PV_HD void ge_basepoint(ge_p3& B) {
 // Table q = 0 serves the generic kernels (q = 4, 2^128 B, the half-size one);
 // the comb kernel of prepared keys uses all eight (B_q = 2^(32 q) B, so
 // S*B = sum_q S_q B_q with the 32-bit words S_q).
-PV_HD void btable_entry(uint32_t* p, int k, int q = 0) {
+PV_HD void btable_entry(uint32_t* p, int k, int q = 0, int nbits = 8) {
   ge_p3 B, acc;
   ge_basepoint(B);
 #pragma unroll 1
@@ -309,7 +309,7 @@ PV_HD void btable_entry(uint32_t* p, int k, int q = 0) {
   ge_cached cb;
   ge_p3_to_cached(cb, B);
   ge_p3_0(acc);
-  for (int bit = 7; bit >= 0; --bit) {
+  for (int bit = nbits - 1; bit >= 0; --bit) {
     ge_p1p1 t;
     ge_p3_dbl(t, acc);
     ge_p1p1_to_p3(acc, t);
@@ -894,6 +894,14 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
 // s' = d S mod L in radix-256 offset form, and a status word
 // (HS_NONE: rejected before the curve, HS_HALF, HS_DEFER) | c_neg << 8.
 constexpr int HREC_WORDS = 20;
+// s' = d S mod L in the curve stage: signed radix-2^16 digits in offset form
+// (+0x8000 per 16-bit digit, one 256-bit add: the carry out of the low 128
+// bits lands in the high half), digit i of the low half from the table of B,
+// of the high half from the table of 2^128 B, both with 2^15 + 1 affine
+// entries k * P (BW_* below; 8.4 MB per device, read from L2/MALL).
+constexpr uint32_t HALF_S_PATTERN = 0x80008000u;
+constexpr int BW_ENTRIES = (1 << 15) + 1;
+constexpr int BW_TABLE = BW_ENTRIES * BT_WORDS;
 constexpr int HREC_C = 0, HREC_D = 5, HREC_S = 10, HREC_FLAGS = 18;
 constexpr int HALF_LANE_WORDS = 2 * AT_WORDS;   // tables of +-A and -R
 
@@ -916,7 +924,7 @@ PV_HD uint32_t lattice_one(uint32_t* rec, bool pre, const uint32_t* dig, const u
         uint32_t S[8], sp[8];
         load8(S, sig + 32);
         sc_mul_small(sp, d, S);
-        sc_add_pattern(sp, sp, 0x80808080u);
+        sc_add_pattern(sp, sp, HALF_S_PATTERN);
         hs_offset(c);
         hs_offset(d);
 #pragma unroll
@@ -934,10 +942,11 @@ PV_HD uint32_t lattice_one(uint32_t* rec, bool pre, const uint32_t* dig, const u
 }
 
 // Q = s' B + c (+-A) + d (-R) over 33 radix-16 windows (c, d) with the
-// radix-256 digits of s' split over the tables of B (low 16 bytes) and
-// 2^128 B (high 16 bytes), both added on even windows.  Horner from the top:
-// per window 4 doublings, one add from each per-lane table, and on even
-// windows two base-point adds.  Leaves the last sum in p1p1 form.
+// signed radix-2^16 digits of s' split over the tables of B (low 128 bits)
+// and 2^128 B (high 128 bits), both added on every fourth window (8 pairs of
+// affine adds instead of 16 with radix 256).  Horner from the top: per window
+// 4 doublings, one add from each per-lane table.  Leaves the last sum in
+// p1p1 form.
 template <int LS = 1>
 PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const uint32_t* rtab, const uint32_t* blo,
                     const uint32_t* bhi) {
@@ -997,23 +1006,46 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
     load_entry<LS>(er, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY * LS, dR < 0);
     ge_add_entry(t, acc, ea, dA < 0);
     ge_p1p1_to_p3(acc, t);
+    // base-point windows (w % 4 == 0): 16-bit digit w / 4 of each half of s';
+    // the low entry is in flight during the -R add, the high one during the
+    // low madd
+    const bool bwin = (w & 3) == 0;
+    const int sh16 = 16 * ((w >> 2) & 1);
+    const int dL = (int)((lw >> sh16) & 0xffffu) - 32768;
+    const int dH = (int)((hw >> sh16) & 0xffffu) - 32768;
+    ge_nentry eb;
+    if (bwin) load_nentry(eb, blo + (dL < 0 ? -dL : dL) * BT_WORDS, dL < 0);
     ge_add_entry(t, acc, er, dR < 0);
+    if (bwin) {
+      ge_p1p1_to_p3(acc, t);
+      ge_nentry ec;
+      load_nentry(ec, bhi + (dH < 0 ? -dH : dH) * BT_WORDS, dH < 0);
+      ge_madd_entry(t, acc, eb, dL < 0);
+      ge_p1p1_to_p3(acc, t);
+      ge_madd_entry(t, acc, ec, dH < 0);
+    }
 #else
     const int dA = (int)((cw >> sh4) & 15u) - 8;
     ge_add_cached_at<LS>(t, acc, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
     ge_p1p1_to_p3(acc, t);
     const int dR = (int)((dw >> sh4) & 15u) - 8;
     ge_add_cached_at<LS>(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY * LS, dR < 0);
-#endif
-    if ((w & 1) == 0) {
-      const int sh8 = 8 * ((w >> 1) & 3);
-      const int dL = (int)((lw >> sh8) & 255u) - 128;
-      const int dH = (int)((hw >> sh8) & 255u) - 128;
+    if ((w & 3) == 0) {
+      // base-point digits: 16-bit digit w / 4 of each half of s' (the
+      // entries come from L2/MALL: each load is issued one step ahead)
+      const int sh16 = 16 * ((w >> 2) & 1);
+      const int dL = (int)((lw >> sh16) & 0xffffu) - 32768;
+      const int dH = (int)((hw >> sh16) & 0xffffu) - 32768;
+      ge_nentry eb;
+      load_nentry(eb, blo + (dL < 0 ? -dL : dL) * BT_WORDS, dL < 0);
       ge_p1p1_to_p3(acc, t);
-      ge_madd_at(t, acc, blo + (dL < 0 ? -dL : dL) * BT_WORDS, dL < 0);
+      ge_nentry ec;
+      load_nentry(ec, bhi + (dH < 0 ? -dH : dH) * BT_WORDS, dH < 0);
+      ge_madd_entry(t, acc, eb, dL < 0);
       ge_p1p1_to_p3(acc, t);
-      ge_madd_at(t, acc, bhi + (dH < 0 ? -dH : dH) * BT_WORDS, dH < 0);
+      ge_madd_entry(t, acc, ec, dH < 0);
     }
+#endif
     if (w == 0) break;
 #if PV_HALF_PREFETCH
     {

@@ -61,11 +61,70 @@ static uint32_t g_btab[BT_CHUNKS * BT_TABLE];
 static uint32_t g_btab_even[4 * BT_TABLE];   // chunks 0, 2, 4, 6 (the keyed kernel's LDS image)
 static int g_btab_ready = 0;
 
+// radix-2^16 tables of B and 2^128 B (the device builds each entry with
+// btable_entry(.., 16); here: k*P = (k-1)*P + P and one batch inversion per
+// table, the same points in affine niels form)
+static uint32_t g_bw[2 * BW_TABLE];
+
+static void build_bw() {
+  static ge_p3 pts[BW_ENTRIES];
+  static fe pre[BW_ENTRIES];
+  for (int t = 0; t < 2; ++t) {
+    ge_p3 P;
+    ge_basepoint(P);
+    for (int d = 0; d < 128 * t; ++d) {
+      ge_p1p1 u;
+      ge_p3_dbl(u, P);
+      ge_p1p1_to_p3(P, u);
+    }
+    ge_cached cp;
+    ge_p3_to_cached(cp, P);
+    ge_p3_0(pts[0]);
+    for (int k = 1; k < BW_ENTRIES; ++k) {
+      ge_p1p1 u;
+      ge_add_cached(u, pts[k - 1], cp, false);
+      ge_p1p1_to_p3(pts[k], u);
+    }
+    fe acc;
+    fe_copy(acc, pts[0].Z);
+    fe_copy(pre[0], acc);
+    for (int k = 1; k < BW_ENTRIES; ++k) {
+      fe_mul(acc, acc, pts[k].Z);
+      fe_copy(pre[k], acc);
+    }
+    fe_invert(acc, acc);
+    fe d2;
+    fe_const_d2(d2);
+    for (int k = BW_ENTRIES - 1; k >= 0; --k) {
+      fe zi, x, y, v;
+      if (k > 0) {
+        fe_mul(zi, acc, pre[k - 1]);
+        fe_mul(acc, acc, pts[k].Z);
+      } else {
+        fe_copy(zi, acc);
+      }
+      fe_mul(x, pts[k].X, zi);
+      fe_mul(y, pts[k].Y, zi);
+      uint32_t* p = g_bw + (uint64_t)t * BW_TABLE + (uint64_t)k * BT_WORDS;
+      fe_add(v, y, x); fe_carry(v);
+      store_fe(p, v);
+      fe_sub(v, y, x); fe_carry(v);
+      store_fe(p + 10, v);
+      fe_mul(v, x, y);
+      fe_mul(v, v, d2);
+      store_fe(p + 20, v);
+      p[30] = 0;
+      p[31] = 0;
+    }
+  }
+}
+
 static void ensure_btab() {
   if (g_btab_ready) return;
   for (int q = 0; q < BT_CHUNKS; ++q)
     for (int k = 0; k < BT_ENTRIES; ++k) btable_entry(g_btab + (q * BT_ENTRIES + k) * BT_WORDS, k, q);
   for (int t = 0; t < 4; ++t) memcpy(g_btab_even + t * BT_TABLE, g_btab + 2 * t * BT_TABLE, 4 * BT_TABLE);
+  build_bw();
   g_btab_ready = 1;
 }
 
@@ -88,7 +147,7 @@ void hc_verify_batch_mode(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
     const uint32_t st = lattice_one(rec, pre, h, sig + 64 * i, force_full != 0);
     bool ok = false;
     if (st == HS_HALF) {
-      ok = curve_half(pk + 32 * i, sig + 64 * i, rec, lane, g_btab, g_btab + 4 * BT_TABLE);
+      ok = curve_half(pk + 32 * i, sig + 64 * i, rec, lane, g_bw, g_bw + BW_TABLE);
     } else if (st == HS_DEFER) {
       ok = verify_full_one(pk + 32 * i, sig + 64 * i, h, lane, g_btab);
       ++nd;
