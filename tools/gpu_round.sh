@@ -15,6 +15,6 @@ step c3 && timeout -k 10 240 python bench.py --config c3 > "$out/bench_c3.json" 
 step c4 && timeout -k 10 300 python bench.py --config c4 --steps 3 --warmup 1 > "$out/bench_c4.json" 2> "$out/bench_c4.err" && \
 step f3 && timeout -k 10 240 python bench.py --config f3 > "$out/bench_f3.json" 2> "$out/bench_f3.err" && \
 step rocprof && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 bench.py --no-cpu-baseline \
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e \
     > "$out/prof.log" 2>&1 && \
 step pmc && bash tools/pmc_passes.sh "$out/pmc" && step done

@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 run() {
   tag=$1; shift
   timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$out/$tag" -o pmc -- \
-    python3 bench.py --steps 1 --warmup 0 --n "$n" --no-cpu-baseline > "$out/$tag.log" 2>&1
+    python3 bench.py --steps 1 --warmup 0 --n "$n" --no-cpu-baseline --no-e2e > "$out/$tag.log" 2>&1
   rc=$?
   echo "pass $tag rc=$rc"
   return $rc
