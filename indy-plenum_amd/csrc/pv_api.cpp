@@ -86,7 +86,7 @@ struct Device {
   int curve_blocks = 0;
   int hash_blocks = 0;
   DevBuf<uint32_t> btab;
-  DevBuf<uint32_t> bw;        // radix-2^16 base-point tables of the half-size path
+  DevBuf<uint32_t> bw;        // radix-2^16 base-point chunk tables (half-size path, keyed comb)
   DevBuf<uint32_t> scratch;   // per-lane A tables for the persistent curve grid
   DevBuf<uint32_t> h;         // SHA-512 digest, 16 words per signature
   DevBuf<unsigned long long> counter;  // hash-kernel work queue
@@ -245,7 +245,7 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
     d.half_ran = true;
   } else {
     HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict,
-                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx));
+                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p));
   }
   if (timed) {
     HIP_OK(hipEventRecord(d.ev[2], s));

@@ -43,7 +43,7 @@ hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blo
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab = nullptr,
-                        const uint32_t* kidx = nullptr);
+                        const uint32_t* kidx = nullptr, const uint32_t* bw = nullptr);
 
 // Half-size scalar path (generic batches, pv_lattice.h):
 //   launch_lattice   h mod L -> (c, d, s') records (HSREC_WORDS words per
@@ -59,9 +59,11 @@ hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t
                           uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks, uint64_t* bitmap,
                           bool force_full, hipStream_t s);
 // btab: the radix-256 base-point tables (deferred full-length tasks); bw:
-// BWTAB_WORDS words, the radix-2^16 tables of B and 2^128 B (launch_bw_init)
+// BWTAB_WORDS words, the radix-2^16 chunk tables k * 2^(32 q) * B, q = 0..7
+// (launch_bw_init; chunks 0 and 4 serve the half-size path, all eight the
+// keyed comb)
 constexpr int BWTAB_ENTRIES = (1 << 15) + 1;
-constexpr uint64_t BWTAB_WORDS = 2ull * BWTAB_ENTRIES * BTAB_WORDS;
+constexpr uint64_t BWTAB_WORDS = 8ull * BWTAB_ENTRIES * BTAB_WORDS;
 hipError_t launch_bw_init(uint32_t* bw, hipStream_t s);
 hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, const uint32_t* rec,
                              const uint32_t* btab, const uint32_t* bw, uint32_t* scratch, uint64_t scratch_lanes,

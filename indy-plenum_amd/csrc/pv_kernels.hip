@@ -148,19 +148,21 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
                                                                         uint8_t* __restrict__ verdict,
                                                                         uint64_t* __restrict__ bitmap, uint64_t n,
                                                                         const uint32_t* __restrict__ ktab,
-                                                                        const uint32_t* __restrict__ kidx) {
-  // generic kernel: table q = 0 (16.5 KB); comb kernel of prepared keys: the
-  // even chunk tables 0, 2, 4, 6 (66 KB; the odd ones are read from global)
+                                                                        const uint32_t* __restrict__ kidx,
+                                                                        const uint32_t* __restrict__ bw) {
+  // generic kernel: radix-256 table q = 0 in LDS (16.5 KB); the comb kernel of
+  // prepared keys reads the radix-2^16 chunk tables bw from L2/MALL
   constexpr int TW = BTAB_ENTRIES * BTAB_WORDS;
-  constexpr int BT_LDS_WORDS = (KEYED ? 4 : 1) * TW;
-  __shared__ uint32_t btab[BT_LDS_WORDS];
-  for (int j = threadIdx.x; j < BT_LDS_WORDS; j += CURVE_BLOCK) btab[j] = btab_g[(j / TW) * 2 * TW + j % TW];
-  __syncthreads();
+  __shared__ uint32_t btab[KEYED ? 1 : TW];
+  if constexpr (!KEYED) {
+    for (int j = threadIdx.x; j < TW; j += CURVE_BLOCK) btab[j] = btab_g[j];
+    __syncthreads();
+  }
   const uint64_t nthreads = (uint64_t)gridDim.x * CURVE_BLOCK;
   const uint64_t gid = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
   uint32_t* lane = scratch + gid * LANE_WORDS;
   for (uint64_t base = 0; base < n; base += CURVE_K * nthreads) {
-    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx, btab_g);
+    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx, bw);
 #pragma unroll
     for (int k = 0; k < CURVE_K; ++k) {
       const uint64_t i = base + (uint64_t)k * nthreads + gid;
@@ -186,18 +188,19 @@ hipError_t curve_occupancy(int* blocks_per_cu, bool keyed) {
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab,
-                        const uint32_t* kidx) {
+                        const uint32_t* kidx, const uint32_t* bw) {
   if (n == 0) return hipSuccess;
   uint64_t need = (n + (uint64_t)CURVE_BLOCK * CURVE_K - 1) / ((uint64_t)CURVE_BLOCK * CURVE_K);
   uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
   if (b * CURVE_BLOCK > scratch_lanes) b = scratch_lanes / CURVE_BLOCK;
   if (b == 0) return hipErrorInvalidValue;
+  if (ktab && !bw) return hipErrorInvalidValue;
   if (ktab)
     hipLaunchKernelGGL(k_curve<true>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
-                       verdict, bitmap, n, ktab, kidx);
+                       verdict, bitmap, n, ktab, kidx, bw);
   else
     hipLaunchKernelGGL(k_curve<false>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
-                       verdict, bitmap, n, nullptr, nullptr);
+                       verdict, bitmap, n, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -266,7 +269,8 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
       uint32_t st = HS_NONE;
       if (i < n) st = rec[HREC_WORDS * i + HREC_FLAGS] & 0xffu;
       bool ok = false;
-      if (st == HS_HALF) ok = curve_half<PV_HALF_LS>(pk + 32 * i, sig + 64 * i, rec + HREC_WORDS * i, scr, bw, bw + BW_TABLE);
+      if (st == HS_HALF)
+        ok = curve_half<PV_HALF_LS>(pk + 32 * i, sig + 64 * i, rec + HREC_WORDS * i, scr, bw, bw + 4 * BW_TABLE);
       const uint64_t ball = __ballot(ok);
       if (i < n && st != HS_DEFER) verdict[i] = ok ? 1 : 0;
       if (lane == 0 && ball) atomicOr(&bitmap[t - full_tasks], (unsigned long long)ball);
@@ -297,11 +301,11 @@ hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t
 
 __global__ __launch_bounds__(64) void k_bw_init(uint32_t* bw) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < 2 * BW_ENTRIES) btable_entry(bw + (uint64_t)g * BT_WORDS, g % BW_ENTRIES, g < BW_ENTRIES ? 0 : 4, 16);
+  if (g < BW_CHUNKS * BW_ENTRIES) btable_entry(bw + (uint64_t)g * BT_WORDS, g % BW_ENTRIES, g / BW_ENTRIES, 16);
 }
 
 hipError_t launch_bw_init(uint32_t* bw, hipStream_t s) {
-  hipLaunchKernelGGL(k_bw_init, dim3((2 * BW_ENTRIES + 63) / 64), dim3(64), 0, s, bw);
+  hipLaunchKernelGGL(k_bw_init, dim3((BW_CHUNKS * BW_ENTRIES + 63) / 64), dim3(64), 0, s, bw);
   return hipGetLastError();
 }
 

@@ -558,6 +558,17 @@ PV_HD bool curve_point(ge_p2& rp, const uint8_t* pk, const uint8_t* sig, const u
 constexpr int COMB_Q = 8;
 constexpr int BT_CHUNKS = 8;            // base-point tables 2^(32 q) B, q = 0..7
 constexpr int BT_TABLE = BT_ENTRIES * BT_WORDS;
+// s' = d S mod L in the curve stage: signed radix-2^16 digits in offset form
+// (+0x8000 per 16-bit digit, one 256-bit add: the carry out of the low 128
+// bits lands in the high half), digit i of the low half from the table of B,
+// of the high half from the table of 2^128 B, both with 2^15 + 1 affine
+// entries k * P.  The device holds BW_CHUNKS such tables, k * 2^(32 q) * B for
+// q = 0..7 (33.5 MB, read from L2/MALL): chunks 0 and 4 serve the half-size
+// path, all eight the comb of prepared keys.
+constexpr uint32_t HALF_S_PATTERN = 0x80008000u;
+constexpr int BW_ENTRIES = (1 << 15) + 1;
+constexpr int BW_TABLE = BW_ENTRIES * BT_WORDS;
+constexpr int BW_CHUNKS = 8;
 constexpr int KT_ENTRY = 32;
 constexpr int KT_TABLE = 9 * KT_ENTRY;
 constexpr int KEY_STATUS = COMB_Q * KT_TABLE;
@@ -677,23 +688,18 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
 }
 
 // R' = hh*(-A) + ss*B from a prepared key (8 comb tables in kt) and the eight
-// base-point tables: even chunks in `bl` (chunk 2t at bl + t * BT_TABLE, LDS in
-// the kernel), odd chunks in `bg` (chunk q at bg + q * BT_TABLE, global).
+// radix-2^16 base-point chunk tables bw + q * BW_TABLE (k * 2^(32 q) * B).
 // Windows w = 7..0 (4 doublings apart): per window one affine add per chunk q
-// with the signed radix-16 digit 8q + w of hh, and on even windows one per
-// chunk with the signed radix-256 digit 4q + w/2 of ss.  The chunk loops are
-// not unrolled (code size); the digit words rotate through static indices.
+// with the signed radix-16 digit 8q + w of hh, and on windows 4 and 0 one per
+// chunk with the signed radix-2^16 digit 2q + w/4 of ss (16 base-point adds;
+// radix 256 needed 32).  Every table entry is fetched one add ahead into
+// ping-pong registers.  The chunk loops are not unrolled (code size); the
+// digit words rotate through static indices.
 PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32_t ss[8], const uint32_t* kt,
-                                  const uint32_t* bl, const uint32_t* bg) {
+                                  const uint32_t* bw) {
   uint32_t hp[8], sp[8];
   sc_add_pattern(hp, hh, 0x88888888u);
-  sc_add_pattern(sp, ss, 0x80808080u);
-  uint32_t se[4], so[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    se[t] = sp[2 * t];
-    so[t] = sp[2 * t + 1];
-  }
+  sc_add_pattern(sp, ss, HALF_S_PATTERN);
   ge_p3 acc;
   ge_p3_0(acc);
   ge_p1p1 t;
@@ -715,7 +721,7 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
       ge_p1p1_to_p3(acc, t);
     }
     const int sh4 = 4 * w;
-    const bool bwin = (w & 1) == 0;
+    const bool bwin = (w & 3) == 0;
 #if PV_COMB_PREFETCH
     // two key adds per trip, ping-ponging the register entries: the entry of
     // the next add (hp[1] holds its digit word; q = 0 of window w - 1 after
@@ -762,23 +768,28 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
     }
 #endif
     if (bwin) {
-      const int sh8 = 8 * (w >> 1);
+      const int sh16 = 4 * w;   // w = 4: high half of each word, w = 0: low half
+      ge_nentry ba, bb;
+      int db = (int)((sp[0] >> sh16) & 0xffffu) - 32768;
+      load_nentry(ba, bw + (db < 0 ? -db : db) * BT_WORDS, db < 0);
 #pragma unroll 1
-      for (int u = 0; u < 4; ++u) {   // even chunks 0, 2, 4, 6
-        const int dB = (int)((se[0] >> sh8) & 255u) - 128;
-        ge_madd_at(t, acc, bl + u * BT_TABLE + (dB < 0 ? -dB : dB) * BT_WORDS, dB < 0);
+      for (int q = 0; q < COMB_Q; q += 2) {
+        const int d1 = (int)((sp[1] >> sh16) & 0xffffu) - 32768;
+        load_nentry(bb, bw + (q + 1) * BW_TABLE + (d1 < 0 ? -d1 : d1) * BT_WORDS, d1 < 0);
+        ge_madd_entry(t, acc, ba, db < 0);
         ge_p1p1_to_p3(acc, t);
-        const uint32_t x = se[0];
-        se[0] = se[1]; se[1] = se[2]; se[2] = se[3]; se[3] = x;
-      }
-#pragma unroll 1
-      for (int u = 0; u < 4; ++u) {   // odd chunks 1, 3, 5, 7
-        const int dB = (int)((so[0] >> sh8) & 255u) - 128;
-        ge_madd_at(t, acc, bg + (2 * u + 1) * BT_TABLE + (dB < 0 ? -dB : dB) * BT_WORDS, dB < 0);
-        if (u < 3) ge_p1p1_to_p3(acc, t);
+        const bool last = q + 2 >= COMB_Q;
+        const int d2 = (int)((sp[2] >> sh16) & 0xffffu) - 32768;
+        if (!last) load_nentry(ba, bw + (q + 2) * BW_TABLE + (d2 < 0 ? -d2 : d2) * BT_WORDS, d2 < 0);
+        ge_madd_entry(t, acc, bb, d1 < 0);
+        if (!last) ge_p1p1_to_p3(acc, t);
         else ge_p1p1_to_p2(r2, t);
-        const uint32_t x = so[0];
-        so[0] = so[1]; so[1] = so[2]; so[2] = so[3]; so[3] = x;
+        db = d2;
+        const uint32_t x0 = sp[0], x1 = sp[1];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) sp[j] = sp[j + 2];
+        sp[6] = x0;
+        sp[7] = x1;
       }
     }
   }
@@ -787,7 +798,7 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
 
 // R' = h(-A) + S B with -A's comb tables taken from a prepared key
 PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, const uint32_t* dig_src,
-                             const uint32_t* bl, const uint32_t* bg) {
+                             const uint32_t* bw) {
   if (!kt[KEY_STATUS]) return false;
   uint32_t hh[8], S[8];
   {
@@ -797,7 +808,7 @@ PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, 
     sc_reduce64(hh, dig);
   }
   load8(S, sig + 32);
-  double_scalarmult_comb(rp, hh, S, kt, bl, bg);
+  double_scalarmult_comb(rp, hh, S, kt, bw);
   return true;
 }
 
@@ -850,7 +861,7 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     bool ok = false;
     if (i < n && pre[i]) {
       if constexpr (KEYED)
-        ok = curve_point_keyed(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, btab, bg);
+        ok = curve_point_keyed(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, bg);
       else
         ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);
     }
@@ -894,14 +905,6 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
 // s' = d S mod L in radix-256 offset form, and a status word
 // (HS_NONE: rejected before the curve, HS_HALF, HS_DEFER) | c_neg << 8.
 constexpr int HREC_WORDS = 20;
-// s' = d S mod L in the curve stage: signed radix-2^16 digits in offset form
-// (+0x8000 per 16-bit digit, one 256-bit add: the carry out of the low 128
-// bits lands in the high half), digit i of the low half from the table of B,
-// of the high half from the table of 2^128 B, both with 2^15 + 1 affine
-// entries k * P (BW_* below; 8.4 MB per device, read from L2/MALL).
-constexpr uint32_t HALF_S_PATTERN = 0x80008000u;
-constexpr int BW_ENTRIES = (1 << 15) + 1;
-constexpr int BW_TABLE = BW_ENTRIES * BT_WORDS;
 constexpr int HREC_C = 0, HREC_D = 5, HREC_S = 10, HREC_FLAGS = 18;
 constexpr int HALF_LANE_WORDS = 2 * AT_WORDS;   // tables of +-A and -R
 

@@ -344,4 +344,4 @@ def test_op_counts_pin_keyed_constants(hc):
     # the decompression multiplies by sqrt(-1) for about half of all keys
     prep_mul = (int(c_many[0]) - int(c_one[0])) / (n - 1)
     assert abs(prep_mul - bench.W_MUL_KEYPREP) <= 1.0
-    assert abs((int(c_one[0]) - prep_mul) / n - bench.W_MUL_KEYED) <= 0.2
+    assert abs((int(c_one[0]) - prep_mul) / n - bench.W_MUL_KEYED) <= 0.2, (int(c_one[0]) - prep_mul) / n

@@ -61,18 +61,18 @@ static uint32_t g_btab[BT_CHUNKS * BT_TABLE];
 static uint32_t g_btab_even[4 * BT_TABLE];   // chunks 0, 2, 4, 6 (the keyed kernel's LDS image)
 static int g_btab_ready = 0;
 
-// radix-2^16 tables of B and 2^128 B (the device builds each entry with
+// radix-2^16 chunk tables k * 2^(32 q) * B (the device builds each entry with
 // btable_entry(.., 16); here: k*P = (k-1)*P + P and one batch inversion per
 // table, the same points in affine niels form)
-static uint32_t g_bw[2 * BW_TABLE];
+static uint32_t g_bw[BW_CHUNKS * BW_TABLE];
 
 static void build_bw() {
   static ge_p3 pts[BW_ENTRIES];
   static fe pre[BW_ENTRIES];
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < BW_CHUNKS; ++t) {
     ge_p3 P;
     ge_basepoint(P);
-    for (int d = 0; d < 128 * t; ++d) {
+    for (int d = 0; d < 32 * t; ++d) {
       ge_p1p1 u;
       ge_p3_dbl(u, P);
       ge_p1p1_to_p3(P, u);
@@ -147,7 +147,7 @@ void hc_verify_batch_mode(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
     const uint32_t st = lattice_one(rec, pre, h, sig + 64 * i, force_full != 0);
     bool ok = false;
     if (st == HS_HALF) {
-      ok = curve_half(pk + 32 * i, sig + 64 * i, rec, lane, g_bw, g_bw + BW_TABLE);
+      ok = curve_half(pk + 32 * i, sig + 64 * i, rec, lane, g_bw, g_bw + 4 * BW_TABLE);
     } else if (st == HS_DEFER) {
       ok = verify_full_one(pk + 32 * i, sig + 64 * i, h, lane, g_btab);
       ++nd;
@@ -216,7 +216,7 @@ void hc_verify_keyed(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const 
   for (uint64_t i = 0; i < n; ++i)
     pre[i] = hash_one(h + 16 * i, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
   for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
-    const uint32_t okm = curve_group<true>(pk, sig, h, pre, i0, 1, n, lane, g_btab_even, ktab, kidx, g_btab);
+    const uint32_t okm = curve_group<true>(pk, sig, h, pre, i0, 1, n, lane, g_btab_even, ktab, kidx, g_bw);
     for (int q = 0; q < CURVE_K && i0 + q < n; ++q) verdict[i0 + q] = (okm >> q) & 1u;
   }
   free(ktab);
