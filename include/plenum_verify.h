@@ -71,7 +71,9 @@ extern "C" {
 #define PV_KEY_WORDS 2312u
 
 /* Initialise the engine on the GPUs in device_mask (bit d = HIP device d;
- * 0 = all visible devices).  Idempotent.  Builds the base-point table. */
+ * 0 = all visible devices).  Idempotent.  Builds the base-point tables
+ * (radix 256, 132 KB; radix 2^16 chunk tables k * 2^(32 q) * B, 33.5 MB per
+ * device). */
 int pv_init(uint32_t device_mask);
 
 /* Release every device resource.  Safe to call when not initialised. */
@@ -89,7 +91,9 @@ int pv_device_count(void);
  *   msg_blob, msg_off  messages (see conventions)
  *   verdict n bytes out, 1 = valid, 0 = invalid
  * The batch is split into contiguous shards over the devices in device_mask
- * (0 = every initialised device). */
+ * (0 = every initialised device); each shard runs as a pipeline of up to 8
+ * chunks (H2D of chunk c+1 on a copy stream overlaps the kernels of chunk c).
+ * Synchronous: returns after every verdict is in `verdict`. */
 int pv_verify_batch(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
                     uint64_t n, uint8_t *verdict, uint32_t device_mask, uint32_t flags);
 
