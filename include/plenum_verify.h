@@ -230,6 +230,21 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
                                 uint64_t *bitmap, int device, void *stream, int iters, float *ms_hash,
                                 float *ms_curve);
 
+/* Host-side staging of pv_verify_batch's inputs, chosen by PV_HOST_STAGING /
+ * PV_HOST_COPY_THREADS at pv_init:
+ *   PV_STAGING_PINNED   ("pinned", default) each chunk is gathered by up to
+ *                       copy_threads host threads into one of two page-locked
+ *                       slots per device and DMA'd from there; verdicts come
+ *                       back through a page-locked buffer;
+ *   PV_STAGING_PAGEABLE ("pageable") the caller's buffers go straight to
+ *                       hipMemcpyAsync (the runtime stages them).
+ * Verdicts are identical either way.  pv_set_host_staging switches every
+ * initialised device (A/B timing, tests); copy_threads 0 keeps the current
+ * count, otherwise 1..64. */
+#define PV_STAGING_PINNED 0u
+#define PV_STAGING_PAGEABLE 1u
+int pv_set_host_staging(uint32_t mode, int copy_threads);
+
 #ifdef __cplusplus
 }
 #endif

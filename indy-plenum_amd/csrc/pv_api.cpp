@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -38,8 +39,13 @@ int fail(int code, const char* fmt, ...) {
 
 // host-buffer pipeline (pv_verify_batch): a shard runs as at most
 // PV_HOST_CHUNKS chunks of at least PV_HOST_CHUNK_MIN signatures
-#define PV_HOST_CHUNKS 8
+#define PV_HOST_CHUNKS 4
 #define PV_HOST_CHUNK_MIN 65536
+// chunk gathers into the pinned staging ring use up to this many host threads
+// (PV_HOST_COPY_THREADS overrides); gathers under PV_HOST_PAR_MIN bytes stay on
+// the calling thread
+#define PV_HOST_COPY_THREADS 8
+#define PV_HOST_PAR_MIN (4u << 20)
 
 #define HIP_OK(expr)                                                                          \
   do {                                                                                        \
@@ -70,6 +76,91 @@ struct DevBuf {
   }
 };
 
+// page-locked host buffer (one slot of the host-buffer staging ring)
+struct PinBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;  // bytes
+  hipError_t ensure(size_t n) {
+    if (n <= cap && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// host -> host copies of one chunk's inputs, split over `threads` threads by
+// byte range of the concatenated jobs
+struct CopyJob {
+  uint8_t* dst;
+  const uint8_t* src;
+  size_t n;
+};
+
+void gather(const CopyJob* jobs, int nj, int threads) {
+  size_t total = 0;
+  for (int j = 0; j < nj; ++j) total += jobs[j].n;
+  auto run = [&](size_t a, size_t b) {
+    size_t base = 0;
+    for (int j = 0; j < nj && base < b; base += jobs[j].n, ++j) {
+      const size_t lo = std::max(a, base), hi = std::min(b, base + jobs[j].n);
+      if (lo < hi) memcpy(jobs[j].dst + (lo - base), jobs[j].src + (lo - base), hi - lo);
+    }
+  };
+  if (threads <= 1 || total < PV_HOST_PAR_MIN) {
+    run(0, total);
+    return;
+  }
+  std::vector<std::thread> ts;
+  ts.reserve(threads - 1);
+  const size_t piece = (total + threads - 1) / threads;
+  for (int t = 1; t < threads; ++t) ts.emplace_back(run, std::min(total, piece * t), std::min(total, piece * (t + 1)));
+  run(0, std::min(total, piece));
+  for (auto& t : ts) t.join();
+}
+
+// Distinct 32-byte keys of a host batch (PV_FLAG_DEDUP_KEYS): open addressing
+// with linear probing over 32-bit slots (0 = empty, else 1 + distinct index),
+// hashed from the key's first 16 bytes; no per-key allocation.
+struct KeyIndex {
+  std::vector<uint32_t> slot;
+  uint64_t mask = 0;
+  const uint8_t* base = nullptr;  // key j at base + 32 * first[j]
+  std::vector<uint64_t> first;    // position of each distinct key's first use
+  void reset(const uint8_t* keys, uint64_t n) {
+    uint64_t cap = 64;
+    while (cap < 2 * n) cap <<= 1;
+    slot.assign(cap, 0);
+    mask = cap - 1;
+    base = keys;
+    first.clear();
+  }
+  // distinct index of key i (inserted on first sight)
+  uint32_t insert(uint64_t i) {
+    const uint8_t* k = base + 32 * i;
+    uint64_t a, b;
+    memcpy(&a, k, 8);
+    memcpy(&b, k + 8, 8);
+    uint64_t h = (a ^ (b * 0x9E3779B97F4A7C15ull)) * 0xBF58476D1CE4E5B9ull;
+    for (uint64_t p = (h >> 17) & mask;; p = (p + 1) & mask) {
+      const uint32_t v = slot[p];
+      if (!v) {
+        first.push_back(i);
+        slot[p] = (uint32_t)first.size();
+        return v + (uint32_t)first.size() - 1;
+      }
+      if (!memcmp(base + 32 * first[v - 1], k, 32)) return v - 1;
+    }
+  }
+};
+
 // PV_CURVE_MODE (read at pv_init): "half" (default) = half-size scalars with
 // full-length tasks for deferred records; "full" = every record deferred
 // (full-length verdicts through the same kernel: A/B timing and tests);
@@ -82,6 +173,15 @@ struct Device {
   hipStream_t stream = nullptr;
   hipStream_t copy = nullptr;   // host-buffer calls: H2D of chunk c+1 overlaps the kernels of chunk c
   hipEvent_t copied = nullptr;  // recorded on `copy` after each chunk's inputs, waited on by `stream`
+  // PV_HOST_STAGING (read at pv_init): "pinned" (default) gathers chunk c of a
+  // host-buffer call into page-locked slot c & 1 and DMAs it from there;
+  // "pageable" hands the caller's buffers to hipMemcpyAsync (runtime staging)
+  bool pinned = true;
+  int copy_threads = PV_HOST_COPY_THREADS;
+  int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
+  PinBuf pin[2];
+  PinBuf vout;  // page-locked verdicts of the shard (D2H target; copied to the caller after the drain)
+  hipEvent_t staged[2] = {nullptr, nullptr};  // slot i's H2D has finished
   int cu_count = 0;
   int curve_blocks = 0;
   int hash_blocks = 0;
@@ -138,6 +238,20 @@ int init_device(Device& d) {
   HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
   HIP_OK(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
+  for (auto& e : d.staged) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (const char* m = getenv("PV_HOST_STAGING")) {
+    if (!strcmp(m, "pageable")) d.pinned = false;
+    else if (strcmp(m, "pinned") != 0) return fail(PV_EINVAL, "PV_HOST_STAGING must be pinned or pageable (got %s)", m);
+  }
+  if (const char* t = getenv("PV_HOST_CHUNKS")) {
+    d.host_chunks = atoi(t);
+    if (d.host_chunks < 1 || d.host_chunks > 256) return fail(PV_EINVAL, "PV_HOST_CHUNKS must be in 1..256 (got %s)", t);
+  }
+  if (const char* t = getenv("PV_HOST_COPY_THREADS")) {
+    d.copy_threads = atoi(t);
+    if (d.copy_threads < 1 || d.copy_threads > 64)
+      return fail(PV_EINVAL, "PV_HOST_COPY_THREADS must be in 1..64 (got %s)", t);
+  }
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d.id));
   d.cu_count = prop.multiProcessorCount;
@@ -200,6 +314,11 @@ void release_device(Device& d) {
   if (d.copied) (void)hipEventDestroy(d.copied);
   d.copied = nullptr;
   if (d.copy) (void)hipStreamSynchronize(d.copy), (void)hipStreamDestroy(d.copy);
+  for (auto& e : d.staged)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
+  d.pin[0].release();
+  d.pin[1].release();
+  d.vout.release();
   d.copy = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d.stream = nullptr;
@@ -327,7 +446,10 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
   // hash + curve and copies the chunk's verdicts back.  The pageable H2D of
   // chunk c + 1 (staged by the runtime on the host thread) then overlaps the
   // kernels of chunk c.  Chunks index into the shard's buffers (offsets stay
-  // shard-relative), so no device buffer is reused while in flight.
+  // shard-relative), so no device buffer is reused while in flight.  With
+  // pinned staging (default) the H2D is a DMA from a page-locked slot: host
+  // threads gather chunk c + 1 into the other slot while chunk c's DMA and
+  // chunk c - 1's kernels run.
   struct Shard {
     uint64_t s = 0, m = 0, chunk = 0;
     std::vector<uint64_t> offs;
@@ -363,26 +485,38 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     // -A) when at least half of the shard's signatures repeat a key
     uint64_t nk = m;
     if (flags & PV_FLAG_DEDUP_KEYS) {
-      struct KeyHash {
-        size_t operator()(const std::string& k) const {
-          uint64_t h;
-          memcpy(&h, k.data(), 8);
-          return (size_t)h;
+      // a sample first: s keys (one at a pseudo-random position in each of s
+      // equal strides, so positions never repeat) from a pool of <= m/2
+      // distinct keys in even use repeat ~s^2/m times; a sample with under a
+      // quarter of that means mostly distinct keys, and the full pass is
+      // skipped (the choice only affects speed, never verdicts)
+      KeyIndex ki;
+      bool dedup = true;
+      if (m >= 4 * PV_HOST_CHUNK_MIN) {
+        uint64_t smp = 8;
+        while (smp * smp < 64 * m) smp <<= 1;  // s >= 8 sqrt(m): ~64 expected repeats at the threshold
+        const uint64_t stride = m / smp;
+        ki.reset(pk + 32 * s, m);
+        for (uint64_t j = 0; j < smp; ++j) {
+          uint64_t x = (j + 1) * 0x9E3779B97F4A7C15ull;
+          x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+          x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+          ki.insert(j * stride + (x ^ (x >> 31)) % stride);
         }
-      };
-      std::unordered_map<std::string, uint32_t, KeyHash> seen;
-      seen.reserve(m);
-      z.idx.resize(m);
-      for (uint64_t k = 0; k < m; ++k) {
-        auto it = seen.emplace(std::string(reinterpret_cast<const char*>(pk + 32 * (s + k)), 32), (uint32_t)seen.size());
-        if (it.second) z.upk.insert(z.upk.end(), pk + 32 * (s + k), pk + 32 * (s + k) + 32);
-        z.idx[k] = it.first->second;
+        dedup = 4 * (smp - ki.first.size()) * m >= smp * smp;
       }
-      nk = seen.size();
-      if (2 * nk > m) {
-        nk = m;
-        z.idx.clear();
-        z.upk.clear();
+      if (dedup) {
+        ki.reset(pk + 32 * s, m);
+        z.idx.resize(m);
+        for (uint64_t k = 0; k < m && 2 * ki.first.size() <= m; ++k) z.idx[k] = ki.insert(k);
+        nk = ki.first.size();
+        if (2 * nk > m) {
+          nk = m;
+          z.idx.clear();
+        } else {
+          z.upk.resize(nk * 32);
+          for (uint64_t j = 0; j < nk; ++j) memcpy(z.upk.data() + 32 * j, pk + 32 * (s + ki.first[j]), 32);
+        }
       }
     }
     z.keyed = !z.idx.empty();
@@ -392,7 +526,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     HIP_OK(d.off.ensure(m + 1));
     HIP_OK(d.verdict.ensure(m));
     // workspaces sized for the largest chunk before anything is in flight
-    z.chunk = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + PV_HOST_CHUNKS - 1) / PV_HOST_CHUNKS);
+    z.chunk = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + d.host_chunks - 1) / d.host_chunks);
     const uint64_t cm = std::min(m, z.chunk);
     HIP_OK(d.h.ensure(cm * 16));
     HIP_OK(d.pre.ensure(cm));
@@ -400,6 +534,16 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     HIP_OK(d.hrec.ensure(cm * pv::HSREC_WORDS));
     HIP_OK(d.dlist.ensure(cm));
     max_chunks = std::max(max_chunks, (m + z.chunk - 1) / z.chunk);
+    if (d.pinned) {  // both staging slots sized for the shard's largest chunk
+      size_t cap = 0;
+      for (uint64_t c0 = 0; c0 < m; c0 += z.chunk) {
+        const uint64_t c1 = std::min(m, c0 + z.chunk), mc = c1 - c0;
+        cap = std::max<size_t>(cap, (mc + 1) * 8 + (z.keyed ? 0 : mc * 32) + mc * 64 + (z.offs[c1] - z.offs[c0]));
+      }
+      HIP_OK(d.pin[0].ensure(cap));
+      HIP_OK(d.pin[1].ensure(cap));
+      HIP_OK(d.vout.ensure(m));
+    }
     HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.copy));
     if (z.keyed) {
       HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
@@ -422,12 +566,32 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
       const uint64_t c1 = std::min(z.m, c0 + z.chunk), mc = c1 - c0;
       HIP_OK(hipSetDevice(d.id));
       const uint64_t b0 = msg_off[z.s], cb0 = z.offs[c0], cbytes = z.offs[c1] - cb0;
-      if (!z.keyed)
-        HIP_OK(hipMemcpyAsync(d.pk.p + 32 * c0, pk + 32 * (z.s + c0), mc * 32, hipMemcpyHostToDevice, d.copy));
-      HIP_OK(hipMemcpyAsync(d.sig.p + 64 * c0, sig + 64 * (z.s + c0), mc * 64, hipMemcpyHostToDevice, d.copy));
-      if (cbytes)
-        HIP_OK(hipMemcpyAsync(d.blob.p + cb0, msg_blob + b0 + cb0, cbytes, hipMemcpyHostToDevice, d.copy));
-      HIP_OK(hipMemcpyAsync(d.off.p + c0, z.offs.data() + c0, (mc + 1) * 8, hipMemcpyHostToDevice, d.copy));
+      const uint8_t* src_off = reinterpret_cast<const uint8_t*>(z.offs.data() + c0);
+      const uint8_t* src_pk = pk + 32 * (z.s + c0);
+      const uint8_t* src_sig = sig + 64 * (z.s + c0);
+      const uint8_t* src_blob = msg_blob ? msg_blob + b0 + cb0 : nullptr;
+      if (d.pinned) {
+        // gather the chunk into slot c & 1 once its previous H2D (chunk c - 2) is done
+        const int slot = (int)(c & 1);
+        if (c >= 2) HIP_OK(hipEventSynchronize(d.staged[slot]));
+        uint8_t* base = d.pin[slot].p;
+        uint8_t *p_off = base, *p_pk = p_off + (mc + 1) * 8, *p_sig = p_pk + (z.keyed ? 0 : mc * 32),
+                *p_blob = p_sig + mc * 64;
+        const CopyJob jobs[4] = {{p_off, src_off, (mc + 1) * 8},
+                                 {p_pk, src_pk, z.keyed ? 0 : mc * 32},
+                                 {p_sig, src_sig, mc * 64},
+                                 {p_blob, src_blob, cbytes}};
+        gather(jobs, 4, d.copy_threads);
+        src_off = p_off;
+        src_pk = p_pk;
+        src_sig = p_sig;
+        src_blob = p_blob;
+      }
+      if (!z.keyed) HIP_OK(hipMemcpyAsync(d.pk.p + 32 * c0, src_pk, mc * 32, hipMemcpyHostToDevice, d.copy));
+      HIP_OK(hipMemcpyAsync(d.sig.p + 64 * c0, src_sig, mc * 64, hipMemcpyHostToDevice, d.copy));
+      if (cbytes) HIP_OK(hipMemcpyAsync(d.blob.p + cb0, src_blob, cbytes, hipMemcpyHostToDevice, d.copy));
+      HIP_OK(hipMemcpyAsync(d.off.p + c0, src_off, (mc + 1) * 8, hipMemcpyHostToDevice, d.copy));
+      if (d.pinned) HIP_OK(hipEventRecord(d.staged[c & 1], d.copy));
       HIP_OK(hipEventRecord(d.copied, d.copy));
       HIP_OK(hipStreamWaitEvent(d.stream, d.copied, 0));
       // blob base + shard-relative offsets: the hash kernel reads blob + off[i]
@@ -435,7 +599,8 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
                               d.verdict.p + c0, nullptr, d.stream, false, nullptr, nullptr,
                               z.keyed ? d.ktab.p : nullptr, z.keyed ? d.kidx.p + c0 : nullptr);
       if (rc) return rc;
-      HIP_OK(hipMemcpyAsync(verdict + z.s + c0, d.verdict.p + c0, mc, hipMemcpyDeviceToHost, d.stream));
+      HIP_OK(hipMemcpyAsync(d.pinned ? d.vout.p + c0 : verdict + z.s + c0, d.verdict.p + c0, mc,
+                            hipMemcpyDeviceToHost, d.stream));
     }
   }
   // drain (the staging vectors in `sh` outlive every copy that reads them)
@@ -443,6 +608,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     HIP_OK(hipSetDevice(devs[g]->id));
     HIP_OK(hipStreamSynchronize(devs[g]->copy));
     HIP_OK(hipStreamSynchronize(devs[g]->stream));
+    if (devs[g]->pinned && sh[g].m) memcpy(verdict + sh[g].s, devs[g]->vout.p, sh[g].m);
   }
   return PV_OK;
 }
@@ -558,6 +724,18 @@ int pv_set_curve_mode(uint32_t mode) {
   for (auto& d : g_devs) {
     d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
     d.half_ran = false;
+  }
+  return PV_OK;
+}
+
+int pv_set_host_staging(uint32_t mode, int copy_threads) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (mode > PV_STAGING_PAGEABLE) return fail(PV_EINVAL, "unknown staging mode %u", mode);
+  if (copy_threads < 0 || copy_threads > 64) return fail(PV_EINVAL, "copy_threads must be in 0..64 (got %d)", copy_threads);
+  for (auto& d : g_devs) {
+    d.pinned = mode == PV_STAGING_PINNED;
+    if (copy_threads) d.copy_threads = copy_threads;
   }
   return PV_OK;
 }

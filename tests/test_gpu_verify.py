@@ -179,9 +179,36 @@ def test_host_pipeline_multi_chunk(nat, shape):
     off = b.off.cpu().numpy().astype(np.uint64)
     blob = b.blob.cpu().numpy()[:int(off[-1])]
     want = ~b.tamper.cpu().numpy().astype(bool)
-    for dedup in (False, True):
+    # pinned staging ring (3 chunks: chunk 2 reuses slot 0 after its DMA) with
+    # threaded and single-thread gathers, and the runtime's pageable staging
+    try:
+        for staging, threads in (('pinned', 8), ('pinned', 1), ('pageable', 0)):
+            nat.set_host_staging(staging, threads)
+            for dedup in (False, True):
+                got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=dedup)
+                assert (got == want).all(), (shape, staging, threads, dedup, int((got != want).sum()))
+            # two full chunks and a 3-signature tail chunk
+            got = nat.verify_batch_arrays(pk[:131075], sig[:131075], blob[:int(off[131075])], off[:131076])
+            assert (got == want[:131075]).all(), (shape, staging, threads)
+    finally:
+        nat.set_host_staging('pinned', 8)
+
+
+@pytest.mark.parametrize('key_mod', [4096, 0])
+def test_host_dedup_sampled(nat, key_mod):
+    """Shards of >= 262144 signatures decide PV_FLAG_DEDUP_KEYS from a key
+    sample first (pooled keys: prepared-key path; distinct keys: full pass
+    skipped).  Verdicts == not tampered either way, pinned staging."""
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch
+    if key_mod:
+        b = SyntheticBatch(0, 300000, 128, cfg=4, first=777, key_mod=key_mod, mode=synth.RANGE, mlen_max=512)
+    else:
+        b = SyntheticBatch(0, 300000, 200, cfg=2, first=31337)
+    pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()
+    off = b.off.cpu().numpy().astype(np.uint64)
+    blob = b.blob.cpu().numpy()[:int(off[-1])]
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    for dedup in (True, False):
         got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=dedup)
-        assert (got == want).all(), (shape, dedup, int((got != want).sum()))
-    # two full chunks and a 3-signature tail chunk
-    got = nat.verify_batch_arrays(pk[:131075], sig[:131075], blob[:int(off[131075])], off[:131076])
-    assert (got == want[:131075]).all()
+        assert (got == want).all(), (key_mod, dedup, int((got != want).sum()))
