@@ -231,7 +231,9 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
                                 float *ms_curve);
 
 /* Host-side staging of pv_verify_batch's inputs, chosen by PV_HOST_STAGING /
- * PV_HOST_COPY_THREADS at pv_init:
+ * PV_HOST_COPY_THREADS / PV_HOST_CHUNKS at pv_init.  A shard runs as a
+ * pipeline of chunks: a short first chunk (half a regular one) so the kernels
+ * start early, then about `chunks` equal chunks of >= 65536 signatures.
  *   PV_STAGING_PINNED   ("pinned", default) each chunk is gathered by up to
  *                       copy_threads host threads into one of two page-locked
  *                       slots per device and DMA'd from there; verdicts come
@@ -239,11 +241,11 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
  *   PV_STAGING_PAGEABLE ("pageable") the caller's buffers go straight to
  *                       hipMemcpyAsync (the runtime stages them).
  * Verdicts are identical either way.  pv_set_host_staging switches every
- * initialised device (A/B timing, tests); copy_threads 0 keeps the current
- * count, otherwise 1..64. */
+ * initialised device (A/B timing, tests); copy_threads / chunks 0 keep the
+ * current value, otherwise 1..64 / 1..256. */
 #define PV_STAGING_PINNED 0u
 #define PV_STAGING_PAGEABLE 1u
-int pv_set_host_staging(uint32_t mode, int copy_threads);
+int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks);
 
 #ifdef __cplusplus
 }

@@ -451,7 +451,8 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
   // threads gather chunk c + 1 into the other slot while chunk c's DMA and
   // chunk c - 1's kernels run.
   struct Shard {
-    uint64_t s = 0, m = 0, chunk = 0;
+    uint64_t s = 0, m = 0;
+    std::vector<uint64_t> bounds;  // chunk c = [bounds[c], bounds[c + 1])
     std::vector<uint64_t> offs;
     std::vector<uint8_t> upk;
     std::vector<uint32_t> idx;
@@ -526,18 +527,30 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     HIP_OK(d.off.ensure(m + 1));
     HIP_OK(d.verdict.ensure(m));
     // workspaces sized for the largest chunk before anything is in flight
-    z.chunk = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + d.host_chunks - 1) / d.host_chunks);
-    const uint64_t cm = std::min(m, z.chunk);
+    // chunk bounds: a short first chunk (half a regular one, >= PV_HOST_CHUNK_MIN)
+    // so the kernels start early, then the rest in equal chunks
+    {
+      const uint64_t reg = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + d.host_chunks - 1) / d.host_chunks);
+      const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg / 2));
+      z.bounds.assign(1, 0);
+      if (d.host_chunks > 1 && first < m) z.bounds.push_back(first);
+      const uint64_t rest = m - z.bounds.back();
+      const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>((rest + reg - 1) / reg, rest / PV_HOST_CHUNK_MIN));
+      const uint64_t b0 = z.bounds.back();
+      for (uint64_t j = 1; j <= k; ++j) z.bounds.push_back(b0 + rest * j / k);
+    }
+    uint64_t cm = 0;
+    for (size_t j = 1; j < z.bounds.size(); ++j) cm = std::max(cm, z.bounds[j] - z.bounds[j - 1]);
     HIP_OK(d.h.ensure(cm * 16));
     HIP_OK(d.pre.ensure(cm));
     HIP_OK(d.bitmap.ensure((cm + 63) / 64));
     HIP_OK(d.hrec.ensure(cm * pv::HSREC_WORDS));
     HIP_OK(d.dlist.ensure(cm));
-    max_chunks = std::max(max_chunks, (m + z.chunk - 1) / z.chunk);
+    max_chunks = std::max<uint64_t>(max_chunks, z.bounds.size() - 1);
     if (d.pinned) {  // both staging slots sized for the shard's largest chunk
       size_t cap = 0;
-      for (uint64_t c0 = 0; c0 < m; c0 += z.chunk) {
-        const uint64_t c1 = std::min(m, c0 + z.chunk), mc = c1 - c0;
+      for (size_t j = 1; j < z.bounds.size(); ++j) {
+        const uint64_t c0 = z.bounds[j - 1], c1 = z.bounds[j], mc = c1 - c0;
         cap = std::max<size_t>(cap, (mc + 1) * 8 + (z.keyed ? 0 : mc * 32) + mc * 64 + (z.offs[c1] - z.offs[c0]));
       }
       HIP_OK(d.pin[0].ensure(cap));
@@ -561,9 +574,9 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     for (uint64_t g = 0; g < G; ++g) {
       Device& d = *devs[g];
       Shard& z = sh[g];
-      const uint64_t c0 = c * z.chunk;
-      if (c0 >= z.m) continue;
-      const uint64_t c1 = std::min(z.m, c0 + z.chunk), mc = c1 - c0;
+      if (c + 1 >= z.bounds.size()) continue;
+      const uint64_t c0 = z.bounds[c];
+      const uint64_t c1 = z.bounds[c + 1], mc = c1 - c0;
       HIP_OK(hipSetDevice(d.id));
       const uint64_t b0 = msg_off[z.s], cb0 = z.offs[c0], cbytes = z.offs[c1] - cb0;
       const uint8_t* src_off = reinterpret_cast<const uint8_t*>(z.offs.data() + c0);
@@ -728,14 +741,16 @@ int pv_set_curve_mode(uint32_t mode) {
   return PV_OK;
 }
 
-int pv_set_host_staging(uint32_t mode, int copy_threads) {
+int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
   if (mode > PV_STAGING_PAGEABLE) return fail(PV_EINVAL, "unknown staging mode %u", mode);
   if (copy_threads < 0 || copy_threads > 64) return fail(PV_EINVAL, "copy_threads must be in 0..64 (got %d)", copy_threads);
+  if (chunks < 0 || chunks > 256) return fail(PV_EINVAL, "chunks must be in 0..256 (got %d)", chunks);
   for (auto& d : g_devs) {
     d.pinned = mode == PV_STAGING_PINNED;
     if (copy_threads) d.copy_threads = copy_threads;
+    if (chunks) d.host_chunks = chunks;
   }
   return PV_OK;
 }

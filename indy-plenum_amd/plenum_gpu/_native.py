@@ -56,7 +56,7 @@ SIGNATURES = [
       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ('pv_curve_stats', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)]),
     ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
-    ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int]),
+    ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
     ('pv_kernel_timing', ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
       ctypes.POINTER(ctypes.c_uint64)]),
@@ -83,10 +83,10 @@ def set_curve_mode(name):
 STAGING_MODES = {0: 'pinned', 1: 'pageable'}   # PV_STAGING_PINNED / _PAGEABLE
 
 
-def set_host_staging(name, copy_threads=0):
+def set_host_staging(name, copy_threads=0, chunks=0):
     """Host-buffer staging of pv_verify_batch on every initialised device (pv_set_host_staging)."""
     code = {v: k for k, v in STAGING_MODES.items()}[name]
-    _check('pv_set_host_staging', load().pv_set_host_staging(code, int(copy_threads)))
+    _check('pv_set_host_staging', load().pv_set_host_staging(code, int(copy_threads), int(chunks)))
 
 
 def curve_stats(device=0):

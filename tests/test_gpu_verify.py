@@ -166,24 +166,26 @@ def test_keyed_device_path_c3_and_c4(nat):
 def test_host_pipeline_multi_chunk(nat, shape):
     """pv_verify_batch runs a shard as a pipeline of chunks (H2D of chunk c+1 on
     the copy stream overlaps the kernels of chunk c; >= 65536 signatures per
-    chunk): a 150k batch spans 3 chunks.  Verdicts == not tampered; the keyed
+    chunk): a 200k batch spans 2-3 chunks.  Verdicts == not tampered; the keyed
     case (4096-key pool, ragged 128 B - 4 KB payloads) indexes the chunk's
     key indices and shard-relative message offsets."""
     from plenum_gpu import synth
     from plenum_gpu.device import SyntheticBatch
     if shape == 'c2':
-        b = SyntheticBatch(0, 150000, 256, cfg=2, first=4242)
+        b = SyntheticBatch(0, 200000, 256, cfg=2, first=4242)
     else:
-        b = SyntheticBatch(0, 150000, 128, cfg=4, first=999, key_mod=4096, mode=synth.RANGE, mlen_max=4096)
+        b = SyntheticBatch(0, 200000, 128, cfg=4, first=999, key_mod=4096, mode=synth.RANGE, mlen_max=4096)
     pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()
     off = b.off.cpu().numpy().astype(np.uint64)
     blob = b.blob.cpu().numpy()[:int(off[-1])]
     want = ~b.tamper.cpu().numpy().astype(bool)
-    # pinned staging ring (3 chunks: chunk 2 reuses slot 0 after its DMA) with
-    # threaded and single-thread gathers, and the runtime's pageable staging
+    # pinned staging ring with threaded and single-thread gathers (4 chunks:
+    # 65536 + 134464 signatures; 16 chunks: 65536 + 2 x 67232, so chunk 2
+    # waits for slot 0's DMA; the tail case below: 65536 + 65539), one chunk,
+    # and the runtime's pageable staging
     try:
-        for staging, threads in (('pinned', 8), ('pinned', 1), ('pageable', 0)):
-            nat.set_host_staging(staging, threads)
+        for staging, threads, chunks in (('pinned', 8, 4), ('pinned', 1, 1), ('pageable', 0, 4), ('pinned', 8, 16)):
+            nat.set_host_staging(staging, threads, chunks)
             for dedup in (False, True):
                 got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=dedup)
                 assert (got == want).all(), (shape, staging, threads, dedup, int((got != want).sum()))
@@ -191,7 +193,7 @@ def test_host_pipeline_multi_chunk(nat, shape):
             got = nat.verify_batch_arrays(pk[:131075], sig[:131075], blob[:int(off[131075])], off[:131076])
             assert (got == want[:131075]).all(), (shape, staging, threads)
     finally:
-        nat.set_host_staging('pinned', 8)
+        nat.set_host_staging('pinned', 8, 4)
 
 
 @pytest.mark.parametrize('key_mod', [4096, 0])
