@@ -46,6 +46,8 @@ int fail(int code, const char* fmt, ...) {
 // the calling thread
 #define PV_HOST_COPY_THREADS 8
 #define PV_HOST_PAR_MIN (4u << 20)
+// largest page-locked staging slot (two per device)
+#define PV_HOST_PIN_MAX (size_t(512) << 20)
 
 #define HIP_OK(expr)                                                                          \
   do {                                                                                        \
@@ -457,6 +459,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     std::vector<uint8_t> upk;
     std::vector<uint32_t> idx;
     bool keyed = false;
+    bool pinned = false;  // this shard's chunks go through the pinned staging ring
   };
   std::vector<Shard> sh(G);
   // on every exit (errors included) wait for the copies that read `sh` and the caller's buffers
@@ -526,19 +529,37 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     HIP_OK(d.blob.ensure(bytes + 16));
     HIP_OK(d.off.ensure(m + 1));
     HIP_OK(d.verdict.ensure(m));
-    // workspaces sized for the largest chunk before anything is in flight
     // chunk bounds: a short first chunk (half a regular one, >= PV_HOST_CHUNK_MIN)
-    // so the kernels start early, then the rest in equal chunks
-    {
-      const uint64_t reg = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + d.host_chunks - 1) / d.host_chunks);
+    // so the kernels start early, then the rest in equal chunks.  With pinned
+    // staging the chunk count doubles until a chunk's inputs fit one
+    // PV_HOST_PIN_MAX slot; a shard whose 65536-signature chunks still do not
+    // fit (or whose page-locked allocation fails) uses pageable staging.
+    auto chunk_bytes = [&](uint64_t c0, uint64_t c1) -> size_t {
+      return (c1 - c0 + 1) * 8 + (z.keyed ? 0 : (c1 - c0) * 32) + (c1 - c0) * 64 + (z.offs[c1] - z.offs[c0]);
+    };
+    size_t cap = 0;
+    for (uint64_t hc = d.host_chunks;; hc *= 2) {
+      const uint64_t reg = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + hc - 1) / hc);
       const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg / 2));
       z.bounds.assign(1, 0);
-      if (d.host_chunks > 1 && first < m) z.bounds.push_back(first);
+      if (hc > 1 && first < m) z.bounds.push_back(first);
       const uint64_t rest = m - z.bounds.back();
       const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>((rest + reg - 1) / reg, rest / PV_HOST_CHUNK_MIN));
       const uint64_t b0 = z.bounds.back();
       for (uint64_t j = 1; j <= k; ++j) z.bounds.push_back(b0 + rest * j / k);
+      cap = 0;
+      for (size_t j = 1; j < z.bounds.size(); ++j) cap = std::max(cap, chunk_bytes(z.bounds[j - 1], z.bounds[j]));
+      if (!d.pinned || cap <= PV_HOST_PIN_MAX || reg == PV_HOST_CHUNK_MIN || hc >= 4096) break;
     }
+    z.pinned = d.pinned && cap <= PV_HOST_PIN_MAX;
+    if (z.pinned && (d.pin[0].ensure(cap) != hipSuccess || d.pin[1].ensure(cap) != hipSuccess ||
+                     d.vout.ensure(m) != hipSuccess)) {
+      (void)hipGetLastError();
+      d.pin[0].release();
+      d.pin[1].release();
+      z.pinned = false;
+    }
+    // workspaces sized for the largest chunk before anything is in flight
     uint64_t cm = 0;
     for (size_t j = 1; j < z.bounds.size(); ++j) cm = std::max(cm, z.bounds[j] - z.bounds[j - 1]);
     HIP_OK(d.h.ensure(cm * 16));
@@ -547,16 +568,6 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     HIP_OK(d.hrec.ensure(cm * pv::HSREC_WORDS));
     HIP_OK(d.dlist.ensure(cm));
     max_chunks = std::max<uint64_t>(max_chunks, z.bounds.size() - 1);
-    if (d.pinned) {  // both staging slots sized for the shard's largest chunk
-      size_t cap = 0;
-      for (size_t j = 1; j < z.bounds.size(); ++j) {
-        const uint64_t c0 = z.bounds[j - 1], c1 = z.bounds[j], mc = c1 - c0;
-        cap = std::max<size_t>(cap, (mc + 1) * 8 + (z.keyed ? 0 : mc * 32) + mc * 64 + (z.offs[c1] - z.offs[c0]));
-      }
-      HIP_OK(d.pin[0].ensure(cap));
-      HIP_OK(d.pin[1].ensure(cap));
-      HIP_OK(d.vout.ensure(m));
-    }
     HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.copy));
     if (z.keyed) {
       HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
@@ -583,7 +594,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
       const uint8_t* src_pk = pk + 32 * (z.s + c0);
       const uint8_t* src_sig = sig + 64 * (z.s + c0);
       const uint8_t* src_blob = msg_blob ? msg_blob + b0 + cb0 : nullptr;
-      if (d.pinned) {
+      if (z.pinned) {
         // gather the chunk into slot c & 1 once its previous H2D (chunk c - 2) is done
         const int slot = (int)(c & 1);
         if (c >= 2) HIP_OK(hipEventSynchronize(d.staged[slot]));
@@ -604,7 +615,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
       HIP_OK(hipMemcpyAsync(d.sig.p + 64 * c0, src_sig, mc * 64, hipMemcpyHostToDevice, d.copy));
       if (cbytes) HIP_OK(hipMemcpyAsync(d.blob.p + cb0, src_blob, cbytes, hipMemcpyHostToDevice, d.copy));
       HIP_OK(hipMemcpyAsync(d.off.p + c0, src_off, (mc + 1) * 8, hipMemcpyHostToDevice, d.copy));
-      if (d.pinned) HIP_OK(hipEventRecord(d.staged[c & 1], d.copy));
+      if (z.pinned) HIP_OK(hipEventRecord(d.staged[c & 1], d.copy));
       HIP_OK(hipEventRecord(d.copied, d.copy));
       HIP_OK(hipStreamWaitEvent(d.stream, d.copied, 0));
       // blob base + shard-relative offsets: the hash kernel reads blob + off[i]
@@ -612,7 +623,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
                               d.verdict.p + c0, nullptr, d.stream, false, nullptr, nullptr,
                               z.keyed ? d.ktab.p : nullptr, z.keyed ? d.kidx.p + c0 : nullptr);
       if (rc) return rc;
-      HIP_OK(hipMemcpyAsync(d.pinned ? d.vout.p + c0 : verdict + z.s + c0, d.verdict.p + c0, mc,
+      HIP_OK(hipMemcpyAsync(z.pinned ? d.vout.p + c0 : verdict + z.s + c0, d.verdict.p + c0, mc,
                             hipMemcpyDeviceToHost, d.stream));
     }
   }
@@ -621,7 +632,7 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
     HIP_OK(hipSetDevice(devs[g]->id));
     HIP_OK(hipStreamSynchronize(devs[g]->copy));
     HIP_OK(hipStreamSynchronize(devs[g]->stream));
-    if (devs[g]->pinned && sh[g].m) memcpy(verdict + sh[g].s, devs[g]->vout.p, sh[g].m);
+    if (sh[g].pinned && sh[g].m) memcpy(verdict + sh[g].s, devs[g]->vout.p, sh[g].m);
   }
   return PV_OK;
 }

@@ -196,6 +196,20 @@ def test_host_pipeline_multi_chunk(nat, shape):
         nat.set_host_staging('pinned', 8, 4)
 
 
+def test_host_staging_slot_cap(nat):
+    """A shard whose smallest chunk (65536 signatures) exceeds one 512 MiB
+    pinned slot runs with pageable staging: 70k x 8 KiB messages (573 MB) in
+    one chunk.  Verdicts == not tampered."""
+    from plenum_gpu.device import SyntheticBatch
+    b = SyntheticBatch(0, 70000, 8192, cfg=2, first=555)
+    pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()
+    off = b.off.cpu().numpy().astype(np.uint64)
+    blob = b.blob.cpu().numpy()[:int(off[-1])]
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=False)
+    assert (got == want).all(), int((got != want).sum())
+
+
 @pytest.mark.parametrize('key_mod', [4096, 0])
 def test_host_dedup_sampled(nat, key_mod):
     """Shards of >= 262144 signatures decide PV_FLAG_DEDUP_KEYS from a key

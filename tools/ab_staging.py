@@ -31,7 +31,7 @@ def main():
             t0 = time.perf_counter()
             nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=dedup)
             ts.append(time.perf_counter() - t0)
-        print(json.dumps({'chunks': os.environ.get('PV_HOST_CHUNKS', '8'), 'staging': staging, 'threads': threads, 'dedup': dedup,
+        print(json.dumps({'chunks': os.environ.get('PV_HOST_CHUNKS', '4'), 'staging': staging, 'threads': threads, 'dedup': dedup,
                           'ms_min': round(min(ts) * 1e3, 3), 'ms_mean': round(sum(ts) / len(ts) * 1e3, 3),
                           'verifies_per_s': round(1e6 / min(ts)), 'mismatches': mism}), flush=True)
     # pooled keys (C4 shape: 2^16-key pool, 128 B - 4 KB) with and without dedup
