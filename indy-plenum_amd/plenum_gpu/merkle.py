@@ -78,3 +78,35 @@ class GpuTreeHasher:
 
     def hash_full_tree(self, leaves):
         return merkle_root(leaves)
+
+    def _hash_full(self, leaves, l_idx, r_idx):
+        """ledger/tree_hasher.py:30-62 TreeHasher._hash_full: (root, hashes) of
+        leaves[l_idx:r_idx], hashes = roots of the full (2^k) subtrees that form
+        the range, largest first ((root,) when the width is a power of two).
+        CompactMerkleTree._push_subtree / extend (ledger/compact_merkle_tree.py:125,
+        183) call it with whole batches of new leaves: each full subtree's
+        root is one GPU Merkle Tree Hash over its leaves, and the range root is
+        their right fold (the split at the largest power of two below the width
+        is exactly the subtree decomposition, so the fold equals the MTH)."""
+        if l_idx < 0 or r_idx < l_idx or r_idx > len(leaves):
+            raise IndexError("{},{} not a valid range over [0,{}]".format(l_idx, r_idx, len(leaves)))
+        width = r_idx - l_idx
+        if width == 0:
+            return self.hash_empty(), ()
+        hashes, a = [], l_idx
+        for bit in range(width.bit_length() - 1, -1, -1):
+            if width >> bit & 1:
+                hashes.append(merkle_root(leaves[a:a + (1 << bit)]))
+                a += 1 << bit
+        hashes = tuple(hashes)
+        if len(hashes) == 1:
+            return hashes[0], hashes
+        return self._hash_fold(hashes), hashes
+
+    def _hash_fold(self, hashes):
+        """ledger/tree_hasher.py:64-69: right fold of hash_children over `hashes`."""
+        rev = iter(hashes[::-1])
+        accum = next(rev)
+        for cur in rev:
+            accum = self.hash_children(cur, accum)
+        return accum

@@ -37,6 +37,40 @@ def test_merkle_roots_match_reference():
         assert th.hash_children(l, r).hex() == fx['children'][k]
 
 
+def test_hash_full_and_compact_tree_extend():
+    """GpuTreeHasher._hash_full / _hash_fold (ledger/tree_hasher.py:30-69) ==
+    the hashlib restatement for ragged ranges (subtree hashes and root), range
+    roots == the reference fixture's roots, and a CompactMerkleTree-style
+    sequence of append/extend calls (ledger/compact_merkle_tree.py:99-193)
+    driven by the GPU hasher keeps the reference CompactMerkleTree's
+    (tree_size, hashes, root) after every call (tests/golden/merkle_compact.json)."""
+    from plenum_gpu.merkle import GpuTreeHasher
+    fx = mk.fixture()
+    leaves, th = fx['leaves'], GpuTreeHasher()
+    roots = {t['size']: t['root'] for t in fx['trees']}
+    for l, r in [(0, 0), (0, 1), (3, 4), (0, 2), (1, 4), (0, 5), (7, 20), (0, 64), (5, 1030), (0, 1030), (512, 1023)]:
+        got = th._hash_full(leaves, l, r)
+        assert got == mk.hash_full(leaves, l, r), (l, r)
+        if l == 0 and r in roots:
+            assert got[0].hex() == roots[r]
+    with pytest.raises(IndexError):
+        th._hash_full(leaves, 3, 2)
+    with pytest.raises(IndexError):
+        th._hash_full(leaves, 0, len(leaves) + 1)
+    gpu, ref = mk.CompactTree(th), mk.CompactTree(mk.HashlibHasher())
+    pos = 0
+    for st in mk.compact_fixture():   # reference CompactMerkleTree states
+        k = st['extend']
+        gpu.extend(leaves[pos:pos + k])
+        ref.extend(leaves[pos:pos + k])
+        pos += k
+        assert (gpu.size, gpu.hashes) == (ref.size, ref.hashes), pos
+        assert gpu.size == st['tree_size'] and [h.hex() for h in gpu.hashes] == st['hashes'], pos
+        assert gpu.root().hex() == st['root'] == ref.root().hex()
+        if pos in roots:
+            assert gpu.root().hex() == roots[pos]
+
+
 def test_request_digests_match_request_key():
     import _ingress_cases as ic
     from plenum_gpu.merkle import request_digests

@@ -47,3 +47,22 @@ def test_levelwise_shape_matches_reference_roots():
         assert mk.mth_levelwise(fx['leaves'][:t['size']]).hex() == t['root'], t['size']
     for i, h in enumerate(fx['leaf_hashes']):
         assert mk.leaf(fx['leaves'][i]).hex() == h
+
+
+def test_compact_tree_restatement_vs_reference_states():
+    """tests/_merkle.py CompactTree + hash_full (the checker the GPU test uses)
+    reproduce the reference CompactMerkleTree's (tree_size, hashes, root) after
+    every append/extend of oracle/gen_compact_merkle.py, and hash_full's roots
+    match the reference TreeHasher roots of tests/golden/merkle.json."""
+    import _merkle as mk
+    fx = mk.fixture()
+    leaves = fx['leaves']
+    for t in fx['trees']:
+        assert mk.hash_full(leaves, 0, t['size'])[0].hex() == t['root'], t['size']
+    tree, pos = mk.CompactTree(mk.HashlibHasher()), 0
+    for st in mk.compact_fixture():
+        tree.extend(leaves[pos:pos + st['extend']])
+        pos += st['extend']
+        assert tree.size == st['tree_size'] == pos
+        assert [h.hex() for h in tree.hashes] == st['hashes']
+        assert tree.root().hex() == st['root'] == mk.mth_levelwise(leaves[:pos]).hex()
