@@ -312,6 +312,7 @@ def main_f3(args):
     # check: root of the same leaves with hashlib (level-wise RFC 6962)
     host = blob[:n * ln].cpu().numpy()
     lvl = [hashlib.sha256(b'\x00' + host[i * ln:(i + 1) * ln].tobytes()).digest() for i in range(n)]
+    leaf_hashes = list(lvl)
     t1 = time.perf_counter()
     while len(lvl) > 1:
         nxt = [hashlib.sha256(b'\x01' + lvl[i] + lvl[i + 1]).digest() for i in range(0, len(lvl) - 1, 2)]
@@ -330,6 +331,22 @@ def main_f3(args):
         lv = nx
     cpu_rate = sample / (time.perf_counter() - t0)
     del t1
+    # CompactMerkleTree.extend's bulk step from host leaves (GpuTreeHasher._hash_full,
+    # ledger/compact_merkle_tree.py:183): n - 1 leaves = one full subtree per set bit
+    from plenum_gpu.merkle import GpuTreeHasher
+    th = GpuTreeHasher()
+    host_leaves = [host[i * ln:(i + 1) * ln].tobytes() for i in range(n - 1)]
+    th._hash_full(host_leaves, 0, n - 1)
+    t0 = time.perf_counter()
+    ext_root, ext_hashes = th._hash_full(host_leaves, 0, n - 1)
+    ext_s = time.perf_counter() - t0
+    lv = leaf_hashes[:n - 1]
+    while len(lv) > 1:
+        nx = [hashlib.sha256(b'\x01' + lv[i] + lv[i + 1]).digest() for i in range(0, len(lv) - 1, 2)]
+        if len(lv) % 2:
+            nx.append(lv[-1])
+        lv = nx
+    mism += int(ext_root != lv[0]) + int(len(ext_hashes) != bin(n - 1).count('1'))
     value = n * args.steps / elapsed
     res = {
         'metric': 'Merkle tree hash leaves/sec (ledger TreeHasher.hash_full_tree, SHA-256)', 'value': round(value, 1),
@@ -340,6 +357,10 @@ def main_f3(args):
                                'RFC 6962 levels), one GPU', 'name': 'f3', 'leaves': n, 'leaf_bytes': ln},
         'verdict_mismatches': mism,
         'input_gbps': round(n * ln * args.steps / elapsed / 1e9, 2),
+        'compact_extend': {'value': round((n - 1) / ext_s, 1), 'unit': 'leaves/s', 'ms': round(ext_s * 1e3, 3),
+                           'path': 'GpuTreeHasher._hash_full over {} host leaves (list of bytes packed once; {} full subtrees, '
+                                   'one pv_merkle_root call each incl. H2D), root checked against '
+                                   'hashlib'.format(n - 1, bin(n - 1).count('1'))},
         'roofline': None,
         'cpu_baseline': {'value': round(cpu_rate, 1), 'unit': 'leaves/s', 'cores': 1, 'kind': 'port',
                          'sample': 'hashlib SHA-256 tree hash (the reference TreeHasher algorithm, level-wise) over '

@@ -5,8 +5,9 @@
   `Request.key` (plenum/common/request.py:82-90) with the native serializer and
   one GPU pass.
 * `GpuTreeHasher` mirrors ledger/tree_hasher.py `TreeHasher` (hash_empty,
-  hash_leaf, hash_children, hash_full_tree) with `hash_full_tree` and
-  `hash_leaves` computed on the GPU (pv_merkle_root): leaf = SHA-256(0x00 || data),
+  hash_leaf, hash_children, hash_full_tree, _hash_full, _hash_fold) with
+  `hash_full_tree`, `hash_leaves` and `_hash_full` (CompactMerkleTree.extend's
+  bulk step) computed on the GPU (pv_merkle_root): leaf = SHA-256(0x00 || data),
   node = SHA-256(0x01 || left || right), RFC 6962 shape.
 
 Like the verify path there is no CPU fallback: the library and a GPU are required.
@@ -93,10 +94,15 @@ class GpuTreeHasher:
         width = r_idx - l_idx
         if width == 0:
             return self.hash_empty(), ()
-        hashes, a = [], l_idx
+        nat.ensure_init()
+        blob, off = _pack(leaves[l_idx:r_idx])   # packed once; each subtree is an offset window
+        lib, hashes, a = nat.load(), [], 0
         for bit in range(width.bit_length() - 1, -1, -1):
             if width >> bit & 1:
-                hashes.append(merkle_root(leaves[a:a + (1 << bit)]))
+                root = np.zeros(32, np.uint8)
+                nat._check('pv_merkle_root', lib.pv_merkle_root(nat._ptr(blob), nat._ptr(off[a:]), 1 << bit,
+                                                                nat._ptr(root), ctypes.c_void_p(0)))
+                hashes.append(root.tobytes())
                 a += 1 << bit
         hashes = tuple(hashes)
         if len(hashes) == 1:
