@@ -1,0 +1,37 @@
+"""Host-buffer latency of pv_verify_batch vs batch size (256 B messages,
+distinct keys, pinned staging): the Looper-pass regime of SURVEY.md 8(b).
+Prints one JSON line per size.  Run on the GPU box:  python tools/latency.py"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'indy-plenum_amd'))
+
+
+def main():
+    from plenum_gpu import _native as nat
+    from plenum_gpu.device import SyntheticBatch
+    nat.ensure_init()
+    b = SyntheticBatch(0, 65536, 256, cfg=2, first=99)
+    pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()
+    off = b.off.cpu().numpy().astype(np.uint64)
+    blob = b.blob.cpu().numpy()[:int(off[-1])]
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    for n in (1, 16, 256, 1024, 4096, 16384, 65536):
+        args = (pk[:n], sig[:n], blob[:int(off[n])], off[:n + 1])
+        got = nat.verify_batch_arrays(*args, dedup_keys=False)
+        ts = []
+        for _ in range(10):
+            t0 = time.perf_counter()
+            nat.verify_batch_arrays(*args, dedup_keys=False)
+            ts.append(time.perf_counter() - t0)
+        print(json.dumps({'n': n, 'ms_min': round(min(ts) * 1e3, 3), 'ms_median': round(sorted(ts)[5] * 1e3, 3),
+                          'verifies_per_s': round(n / min(ts)), 'mismatches': int((got != want[:n]).sum())}),
+              flush=True)
+
+
+if __name__ == '__main__':
+    main()
