@@ -120,11 +120,28 @@ void gather(const CopyJob* jobs, int nj, int threads) {
     run(0, total);
     return;
   }
+  // no exception crosses the ABI: a thread that cannot be started leaves its
+  // range to the calling thread
   std::vector<std::thread> ts;
-  ts.reserve(threads - 1);
+  std::vector<std::pair<size_t, size_t>> left;
   const size_t piece = (total + threads - 1) / threads;
-  for (int t = 1; t < threads; ++t) ts.emplace_back(run, std::min(total, piece * t), std::min(total, piece * (t + 1)));
+  try {
+    ts.reserve(threads - 1);
+    left.reserve(threads);
+  } catch (...) {
+    run(0, total);
+    return;
+  }
+  for (int t = 1; t < threads; ++t) {
+    const size_t a = std::min(total, piece * t), b = std::min(total, piece * (t + 1));
+    try {
+      ts.emplace_back(run, a, b);
+    } catch (...) {
+      left.emplace_back(a, b);
+    }
+  }
   run(0, std::min(total, piece));
+  for (auto& r : left) run(r.first, r.second);
   for (auto& t : ts) t.join();
 }
 
