@@ -268,7 +268,66 @@ PyObject* serialize(PyObject*, PyObject* args) {
   return PyBytes_FromStringAndSize(out.data(), (Py_ssize_t)out.size());
 }
 
+// pack(list|tuple of bytes-like) -> (blob bytes, offsets bytes: n+1 little-endian u64)
+// the message layout of pv_verify_batch / pv_sha256_batch / pv_merkle_root.  Any
+// item without a C-contiguous buffer raises Fallback (the Python packer runs).
+PyObject* pack(PyObject*, PyObject* seq) {
+  if (!PyList_CheckExact(seq) && !PyTuple_CheckExact(seq)) return fallback();
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject** items = PySequence_Fast_ITEMS(seq);
+  PyObject* off = PyBytes_FromStringAndSize(nullptr, (n + 1) * 8);
+  if (!off) return nullptr;
+  uint64_t* o = reinterpret_cast<uint64_t*>(PyBytes_AS_STRING(off));
+  o[0] = 0;
+  bool all_bytes = true;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    Py_ssize_t len;
+    if (PyBytes_CheckExact(items[i])) {
+      len = PyBytes_GET_SIZE(items[i]);
+    } else {
+      all_bytes = false;
+      Py_buffer b;
+      if (PyObject_GetBuffer(items[i], &b, PyBUF_C_CONTIGUOUS) < 0) {
+        PyErr_Clear();
+        Py_DECREF(off);
+        return fallback();
+      }
+      len = b.len;
+      PyBuffer_Release(&b);
+    }
+    o[i + 1] = o[i] + (uint64_t)len;
+  }
+  PyObject* blob = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)o[n]);
+  if (!blob) {
+    Py_DECREF(off);
+    return nullptr;
+  }
+  char* dst = PyBytes_AS_STRING(blob);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    if (all_bytes || PyBytes_CheckExact(items[i])) {
+      memcpy(dst + o[i], PyBytes_AS_STRING(items[i]), o[i + 1] - o[i]);
+      continue;
+    }
+    Py_buffer b;
+    // a buffer whose size changed since the first pass is not packed here
+    if (PyObject_GetBuffer(items[i], &b, PyBUF_C_CONTIGUOUS) < 0 || (uint64_t)b.len != o[i + 1] - o[i]) {
+      if (PyErr_Occurred()) PyErr_Clear();
+      else PyBuffer_Release(&b);
+      Py_DECREF(off);
+      Py_DECREF(blob);
+      return fallback();
+    }
+    memcpy(dst + o[i], b.buf, (size_t)b.len);
+    PyBuffer_Release(&b);
+  }
+  PyObject* r = PyTuple_Pack(2, blob, off);
+  Py_DECREF(blob);
+  Py_DECREF(off);
+  return r;
+}
+
 PyMethodDef kMethods[] = {
+    {"pack", pack, METH_O, "pack a list of bytes-like messages -> (blob, u64 offsets)"},
     {"b58decode", b58decode, METH_O, "base58 decode (str or bytes) -> bytes"},
     {"b58encode", b58encode, METH_O, "base58 encode (bytes or str) -> bytes"},
     {"serialize", serialize, METH_VARARGS, "canonical signing serialization -> UTF-8 bytes"},

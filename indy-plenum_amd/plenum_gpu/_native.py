@@ -167,8 +167,22 @@ def _ptr(a):
     return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else ctypes.c_void_p(0)
 
 
+try:  # native host preprocessing (csrc/pv_host.cpp); the Python packer covers its Fallback cases
+    from . import _host
+except ImportError:
+    _host = None
+
+
 def pack_messages(msgs):
-    """list[bytes] -> (blob uint8, off uint64[n+1])."""
+    """list[bytes] -> (blob uint8, off uint64[n+1]).  Native single pass
+    (plenum_gpu._host.pack) for lists/tuples of bytes-like items; anything else
+    takes the Python packer below."""
+    if _host is not None and type(msgs) in (list, tuple):
+        try:
+            blob, off = _host.pack(msgs)
+            return np.frombuffer(blob, np.uint8), np.frombuffer(off, np.uint64)
+        except _host.Fallback:
+            pass
     n = len(msgs)
     off = np.zeros(n + 1, dtype=np.uint64)
     if n:

@@ -78,3 +78,30 @@ def test_serializer_identical(case, ignore):
     if want[0] == 'ok' and isinstance(obj, float) and obj != obj:
         assert got == want
     assert got == want
+
+
+def test_pack_matches_python_packer():
+    """plenum_gpu._host.pack (csrc/pv_host.cpp) == the Python packer for lists and
+    tuples of bytes-like items (bytes, bytearray, memoryview, contiguous numpy);
+    anything else raises Fallback so pack_messages keeps the Python behaviour."""
+    import numpy as np
+    from plenum_gpu import _host, _native as nat
+
+    def py_pack(msgs):
+        n = len(msgs)
+        off = np.zeros(n + 1, np.uint64)
+        if n:
+            off[1:] = np.cumsum([len(m) for m in msgs])
+        return np.frombuffer(b''.join(msgs), np.uint8), off
+
+    rng = np.random.default_rng(5)
+    cases = [[], [b''], [b'abc'], (b'q', b'', b'zz'),
+             [b'a', bytearray(b'xyz'), memoryview(b'12345'), np.arange(7, dtype=np.uint8)],
+             [rng.bytes(int(k)) for k in rng.integers(0, 600, 500)]]
+    for c in cases:
+        b1, o1 = nat.pack_messages(c)
+        b2, o2 = py_pack([bytes(m) for m in c])
+        assert o1.dtype == np.uint64 and (o1 == o2).all() and (b1 == b2).all()
+    for bad in ([1, 2], [b'a', 'str'], [np.arange(6, dtype=np.uint8)[::2]], iter([b'a'])):
+        with pytest.raises(_host.Fallback):
+            _host.pack(bad)
