@@ -271,10 +271,23 @@ PyObject* serialize(PyObject*, PyObject* args) {
 // pack(list|tuple of bytes-like) -> (blob bytes, offsets bytes: n+1 little-endian u64)
 // the message layout of pv_verify_batch / pv_sha256_batch / pv_merkle_root.  Any
 // item without a C-contiguous buffer raises Fallback (the Python packer runs).
+// The items are snapshotted into a tuple holding strong references first: a
+// buffer provider (PyObject_GetBuffer) may run Python code that mutates the
+// caller's list, and the packer must never read a borrowed pointer after that.
+PyObject* pack_items(PyObject* snap);
+
 PyObject* pack(PyObject*, PyObject* seq) {
   if (!PyList_CheckExact(seq) && !PyTuple_CheckExact(seq)) return fallback();
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
-  PyObject** items = PySequence_Fast_ITEMS(seq);
+  PyObject* snap = PySequence_Tuple(seq);
+  if (!snap) return nullptr;
+  PyObject* r = pack_items(snap);
+  Py_DECREF(snap);
+  return r;
+}
+
+PyObject* pack_items(PyObject* snap) {
+  const Py_ssize_t n = PyTuple_GET_SIZE(snap);
+  PyObject** items = &PyTuple_GET_ITEM(snap, 0);
   PyObject* off = PyBytes_FromStringAndSize(nullptr, (n + 1) * 8);
   if (!off) return nullptr;
   uint64_t* o = reinterpret_cast<uint64_t*>(PyBytes_AS_STRING(off));

@@ -63,12 +63,16 @@ def get_target_verkey(req: dict):
 
 class _VerdictCache:
     """(raw pk, sig||msg) -> verdict, filled by a batch prefetch and consumed
-    by the per-request replay."""
+    by the per-request replay.  Bounded: a prefetch that would grow it past
+    MAX_ITEMS first forgets every older verdict (a miss only costs a verify)."""
+    MAX_ITEMS = 1 << 20
 
     def __init__(self):
         self._d = {}
 
     def fill(self, items, verdicts):
+        if len(self._d) + len(items) > self.MAX_ITEMS:
+            self._d.clear()
         for item, ok in zip(items, verdicts):
             self._d[item] = bool(ok)
 

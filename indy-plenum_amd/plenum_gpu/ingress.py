@@ -13,12 +13,15 @@ every PROPAGATE of it.
 service pass received it collects every request that `verifySignature` would
 authenticate (client requests, PROPAGATE.request, both also inside BATCHes),
 keys them by `Request.key` (plenum/common/request.py:82-120), drops duplicates,
-and runs ONE `ReqAuthenticator.verify_batch` — one GPU pass.  Accepted requests
-land in the authenticator's verified-request cache, so the per-message
-`authenticate(req, key)` that follows short-circuits for them
-(req_authenticator.py:34-35); rejected ones go through the normal path and
-raise the reference's exception there.  Message order, handlers and outcomes
-are unchanged; only where the signature work happens moves.
+and runs ONE `ReqAuthenticator.prefetch` — one GPU pass.  The pre-pass only
+computes signature VERDICTS: it authenticates nothing and never writes the
+verified-request cache (`_verified_reqs`).  The node's unchanged per-message
+path — blacklist check, static validation, then `verifySignature` ->
+`authenticate(req, key)` (node.py:1625-1657) — consumes those verdicts instead
+of calling the verifier, and so fills `_verified_reqs` exactly when and as the
+reference does; a request a handler drops before authenticating leaves no trace.
+Verdicts the pass did not consume are dropped at its end.  Message order,
+handlers and outcomes are unchanged; only where the signature work happens moves.
 """
 import json
 from hashlib import sha256
@@ -137,18 +140,19 @@ class BatchIngress:
 
     # ------------------------------------------------------------ the pass
     def prefetch(self, wrapped: Iterable[Tuple[dict, str]], from_node: bool = False):
-        """One GPU verification pass over the pass's distinct requests; fills
-        the authenticator's verified-request cache.  Returns [identifiers | exception]
-        per distinct request (the outcomes the per-message path will see)."""
+        """One GPU verification pass over the signatures of the pass's distinct
+        requests; the verdicts wait in the authenticators for the per-message
+        `authenticate` calls (nothing is authenticated here).  Returns the
+        distinct (requests, keys); call `end_pass()` after the handlers ran."""
         wrapped = list(wrapped)
         reqs, keys = self.collect(wrapped, from_node)
         self.last_pass.update(messages=len(wrapped), distinct=len(reqs))
-        if not reqs:
-            self.last_pass['verified'] = 0
-            return []
-        res = self.authenticator.verify_batch(reqs, keys)
-        self.last_pass['verified'] = sum(1 for r in res if not isinstance(r, BaseException))
-        return res
+        self.last_pass['verified'] = self.authenticator.prefetch(reqs, keys) if reqs else 0
+        return reqs, keys
+
+    def end_pass(self):
+        """Drop the verdicts of the pass no handler consumed."""
+        self.authenticator.drop_prefetched()
 
     def service(self, wrapped: Iterable[Tuple[dict, str]], handler: Callable, from_node: bool = False,
                 limit: Optional[int] = None) -> int:
@@ -160,8 +164,11 @@ class BatchIngress:
         if limit is not None:
             wrapped = wrapped[:limit]
         self.prefetch(wrapped, from_node)
-        for w in wrapped:
-            handler(w)
+        try:
+            for w in wrapped:
+                handler(w)
+        finally:
+            self.end_pass()
         return len(wrapped)
 
 

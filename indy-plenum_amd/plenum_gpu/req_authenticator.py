@@ -1,13 +1,19 @@
 """Authenticator registry + verified-request cache
-(plenum/server/req_authenticator.py:11-72) with a batch entry point.
+(plenum/server/req_authenticator.py:11-72) with batch entry points.
 
 `verify_batch(reqs, keys)` lets every registered authenticator that supports
 it prefetch GPU verdicts for the requests it would handle, then runs the
-unchanged per-request `authenticate(req, key)` on each.  Accepted requests land
-in `_verified_reqs`, so the node's later per-message `authenticate` calls for
-the same (key, signature) short-circuit exactly as they do after a cache hit
-in the reference (:34-35, :53-57).  Rejected requests surface the same
-exception the per-request path raises.
+unchanged per-request `authenticate(req, key)` on each: it IS a batch of
+`authenticate` calls, so accepted requests land in `_verified_reqs` exactly as
+they would after per-request calls (:34-35, :53-57), and rejected requests
+surface the same exception the per-request path raises.
+
+`prefetch(reqs, keys)` only fills the authenticators' (pk, sig||msg) verdict
+caches and authenticates nothing: `_verified_reqs` keeps being written solely
+by the node's own `authenticate(req, key)` calls, i.e. after its blacklist and
+static-validation checks (node.py:1625-1657).  `drop_prefetched()` forgets the
+verdicts no handler consumed.  This is the form a service pass uses
+(plenum_gpu.ingress.BatchIngress).
 """
 from copy import deepcopy
 from typing import Optional
@@ -45,12 +51,15 @@ class ReqAuthenticator:
         entry = self._verified_reqs.get(key)
         return entry is not None and req_data.get(SIGNATURE) == entry['signature']
 
-    def verify_batch(self, reqs, keys=None):
-        """Authenticate a batch: one GPU verification pass per authenticator,
-        then the per-request path.  Returns [identifiers set | exception]."""
+    def prefetch(self, reqs, keys=None):
+        """One GPU verification pass per authenticator over the signatures of
+        `reqs` it would check; verdicts are kept for the per-request path and
+        nothing is authenticated or cached in `_verified_reqs`.  Returns the
+        number of signatures verified."""
         keys = list(keys) if keys is not None else [None] * len(reqs)
         if len(keys) != len(reqs):
             raise ValueError('keys must match reqs')
+        n = 0
         for authnr in self._authenticators:
             prefetch = getattr(authnr, 'verify_batch', None)
             if prefetch is None:
@@ -63,17 +72,28 @@ class ReqAuthenticator:
                 if authnr.is_write(typ) or authnr.is_action(typ):
                     mine.append(req)
             if mine:
-                prefetch(mine)
+                n += prefetch(mine) or 0
+        return n
+
+    def drop_prefetched(self):
+        """Forget prefetched verdicts no `authenticate` consumed."""
+        for authnr in self._authenticators:
+            drop = getattr(authnr, 'drop_prefetched', None)
+            if drop is not None:
+                drop()
+
+    def verify_batch(self, reqs, keys=None):
+        """Authenticate a batch: one GPU verification pass per authenticator,
+        then the per-request path.  Returns [identifiers set | exception]."""
+        keys = list(keys) if keys is not None else [None] * len(reqs)
+        self.prefetch(reqs, keys)
         out = []
         for req, key in zip(reqs, keys):
             try:
                 out.append(self.authenticate(req, key=key))
             except Exception as ex:
                 out.append(ex)
-        for authnr in self._authenticators:
-            drop = getattr(authnr, 'drop_prefetched', None)
-            if drop is not None:
-                drop()
+        self.drop_prefetched()
         return out
 
     @property

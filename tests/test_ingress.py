@@ -44,3 +44,37 @@ def test_collect_dedups_by_request_key():
     distinct = {c['key'] for c in fx['cases'][::3]}
     assert set(keys) == distinct and len(keys) == len(distinct)
     assert ing.last_pass['requests'] == len(fx['propagates']) + sum(len(b['messages']) for b in fx['batches'])
+
+
+def test_prefetch_never_caches_unauthenticated(monkeypatch):
+    """Host logic of the pre-pass: prefetch only fills verdict
+    caches; `_verified_reqs` is written by the per-message authenticate alone,
+    and a pass's unconsumed verdicts are dropped at its end.  The verifier is
+    stubbed (all accepted) — this checks cache bookkeeping, not verdicts."""
+    import numpy as np
+    from plenum_gpu import nacl_wrappers
+    from plenum_gpu.ingress import BatchIngress, request_key
+    fx = ic.load()
+    ra = ic.make_ra(fx)
+    ing = BatchIngress(ra)
+    calls = []
+
+    def stub(items):
+        calls.append(len(items))
+        return np.ones(len(items), bool)
+    monkeypatch.setattr(nacl_wrappers, 'verify_signed_batch', stub)
+    client, _ = ic.service_pass(fx)
+    # every handler drops its message before verifySignature
+    ing.service(client, lambda w: None)
+    assert len(calls) == 1 and calls[0] > 0
+    assert ra._verified_reqs == {}
+    assert all(not a._verdicts()._d for a in ra._authenticators)
+    # a handler that authenticates one request caches exactly that one
+    first = fx['cases'][0]['req']
+
+    def one(w):
+        if w[0] is client[0][0]:
+            ra.authenticate(w[0], key=request_key(w[0]))
+    ing.service(client, one)
+    assert list(ra._verified_reqs) == [request_key(first)]
+    assert len(calls) == 2          # served from the pass's prefetched verdicts
