@@ -21,7 +21,11 @@
  *                    the Python glue (plenum_gpu.nacl_wrappers) does it.
  *   pv_tally         replaces the per-3PC-batch voter-set count of
  *                    plenum/server/models.py:16-114 (Commits/Prepares.addVote +
- *                    hasQuorum) with quorum values from plenum/server/quorums.py:15-39.
+ *                    hasQuorum) with quorum values from plenum/server/quorums.py:15-39:
+ *                    the SURVEY.md §8(b) contract (node-indexed voter bitmaps);
+ *   pv_tally_votes   the same predicate built from per-message verdicts and sender
+ *                    indices (the voter set is formed on the GPU; also the PROPAGATE
+ *                    f+1 count of plenum/server/propagator.py:38-46).
  *   pv_sign_batch    batch counterpart of SigningKey(seed) + sign
  *                    (stp_core/crypto/nacl_wrappers.py:130-176; crypto_sign_seed_keypair
  *                    + crypto_sign_detached).  Used to generate fixtures/bench data.
@@ -138,18 +142,35 @@ int pv_merkle_root(const uint8_t *blob, const uint64_t *off, uint64_t n, uint8_t
 int pv_merkle_root_device(const uint8_t *blob, const uint64_t *off, uint64_t n, uint8_t *leaf_hashes, uint8_t *root,
                           int device, void *stream);
 
-/* Per-batch quorum tally (HOST memory).
+/* Per-batch quorum tally, SURVEY.md §8(b) form (HOST memory).
+ *   verdict_bits  n_batches x W words, W = ceil(n_nodes / 32): bit j of word w of
+ *                 batch b = node 32 w + j cast a valid vote in batch b (a voter SET:
+ *                 a node's repeated votes are one bit, plenum/server/models.py:24-28)
+ *   dup_mask      same shape, may be NULL: nodes whose votes must not count
+ *                 (e.g. a sender the caller already counted elsewhere)
+ *   reached       n_batches out: popcount(verdict_bits & ~dup_mask) >= quorum
+ * Bits of nodes >= n_nodes are ignored. */
+int pv_tally(const uint32_t *verdict_bits, const uint32_t *dup_mask, uint64_t n_batches, uint32_t n_nodes,
+             uint32_t quorum, uint8_t *reached);
+
+/* DEVICE buffers; votes (may be NULL) receives the per-batch counts. */
+int pv_tally_device(const uint32_t *verdict_bits, const uint32_t *dup_mask, uint64_t n_batches, uint32_t n_nodes,
+                    uint32_t quorum, uint8_t *reached, uint32_t *votes, int device, void *stream);
+
+/* Per-batch quorum tally from per-message verdicts (HOST memory).
  *   verdict    n_msgs bytes (1 = vote counts)
- *   sender     n_msgs node indices (< n_nodes <= 1024)
+ *   sender     n_msgs node indices (< n_nodes <= 1024; an index >= n_nodes is
+ *              PV_EINVAL, never a silently dropped vote)
  *   batch_off  n_batches + 1 offsets into verdict/sender
  *   votes      n_batches out: distinct valid senders per batch
  *   reached    n_batches out: votes >= quorum
  * Duplicate senders count once (a voter SET, plenum/server/models.py:24-28). */
-int pv_tally(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off, uint64_t n_batches,
-             uint32_t n_nodes, uint32_t quorum, uint32_t *votes, uint8_t *reached);
+int pv_tally_votes(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off, uint64_t n_batches,
+                   uint32_t n_nodes, uint32_t quorum, uint32_t *votes, uint8_t *reached);
 
-int pv_tally_device(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off, uint64_t n_batches,
-                    uint32_t n_nodes, uint32_t quorum, uint32_t *votes, uint8_t *reached, int device, void *stream);
+int pv_tally_votes_device(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off,
+                          uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t *votes, uint8_t *reached,
+                          int device, void *stream);
 
 /* Batch keygen + sign (HOST memory): pk_out[i], sig_out[i] for seed i over
  * message i.  Deterministic (RFC 8032 / crypto_sign_detached). */

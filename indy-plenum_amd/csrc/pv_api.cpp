@@ -214,6 +214,7 @@ struct Device {
   DevBuf<uint8_t> pk, sig, blob, verdict, tamper;
   DevBuf<uint64_t> off, bitmap, batch_off;
   DevBuf<uint32_t> sender, votes;
+  DevBuf<uint32_t> tflag, tbits;  // tally: out-of-range sender flag; staged voter bitmaps
   DevBuf<uint8_t> reached;
   DevBuf<uint64_t> scan;      // block sums of the device prefix scan
   DevBuf<uint32_t> ktab, kidx;  // prepared keys + per-signature key index (deduplicated host batches)
@@ -325,7 +326,7 @@ void release_device(Device& d) {
   d.btab.release(); d.bw.release(); d.scratch.release(); d.h.release(); d.pre.release(); d.counter.release();
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.bitmap.release(); d.batch_off.release();
-  d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release();
+  d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release(); d.tflag.release(); d.tbits.release();
   d.ktab.release(); d.kidx.release(); d.kscr.release(); d.mk0.release(); d.mk1.release();
   d.hrec.release(); d.dlist.release(); d.qc.release();
   for (auto& e : d.ev)
@@ -801,22 +802,30 @@ int pv_curve_stats(int device, uint32_t* mode, uint64_t* deferred) {
   return PV_OK;
 }
 
-int pv_tally_device(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
-                    uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached, int device, void* stream) {
+int pv_tally_votes_device(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off,
+                          uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached,
+                          int device, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceGuard dg;
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (n_nodes == 0 || n_nodes > 1024) return fail(PV_EINVAL, "n_nodes must be in 1..1024");
+  if (n_batches == 0) return PV_OK;
+  if (!verdict || !sender || !batch_off || !votes || !reached) return fail(PV_EINVAL, "null device buffer");
   HIP_OK(hipSetDevice(device));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
-  HIP_OK(pv::launch_tally(verdict, sender, batch_off, n_batches, n_nodes, quorum, votes, reached, s));
+  HIP_OK(d->tflag.ensure(1));
+  HIP_OK(hipMemsetAsync(d->tflag.p, 0, 4, s));
+  HIP_OK(pv::launch_tally(verdict, sender, batch_off, n_batches, n_nodes, quorum, votes, reached, d->tflag.p, s));
+  uint32_t bad = 0;
+  HIP_OK(hipMemcpyAsync(&bad, d->tflag.p, 4, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  if (bad) return fail(PV_EINVAL, "a sender index is >= n_nodes (%u)", n_nodes);
   return PV_OK;
 }
 
-int pv_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
-             uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached) {
+int pv_tally_votes(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
+                   uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached) {
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceGuard dg;
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
@@ -831,19 +840,62 @@ int pv_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* bat
     if (k && batch_off[k] < batch_off[k - 1]) return fail(PV_EINVAL, "batch_off not monotone");
     offs[k] = batch_off[k] - b0;
   }
+  for (uint64_t k = 0; k < m; ++k)
+    if (sender[b0 + k] >= n_nodes)
+      return fail(PV_EINVAL, "sender[%llu] = %u is >= n_nodes (%u)", (unsigned long long)(b0 + k), sender[b0 + k],
+                  n_nodes);
   HIP_OK(d.verdict.ensure(m ? m : 1));
   HIP_OK(d.sender.ensure(m ? m : 1));
   HIP_OK(d.batch_off.ensure(n_batches + 1));
   HIP_OK(d.votes.ensure(n_batches));
   HIP_OK(d.reached.ensure(n_batches));
+  HIP_OK(d.tflag.ensure(1));
   if (m) {
     HIP_OK(hipMemcpyAsync(d.verdict.p, verdict + b0, m, hipMemcpyHostToDevice, d.stream));
     HIP_OK(hipMemcpyAsync(d.sender.p, sender + b0, m * 4, hipMemcpyHostToDevice, d.stream));
   }
   HIP_OK(hipMemcpyAsync(d.batch_off.p, offs.data(), (n_batches + 1) * 8, hipMemcpyHostToDevice, d.stream));
   HIP_OK(pv::launch_tally(d.verdict.p, d.sender.p, d.batch_off.p, n_batches, n_nodes, quorum, d.votes.p, d.reached.p,
-                          d.stream));
+                          d.tflag.p, d.stream));
   HIP_OK(hipMemcpyAsync(votes, d.votes.p, n_batches * 4, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipMemcpyAsync(reached, d.reached.p, n_batches, hipMemcpyDeviceToHost, d.stream));
+  HIP_OK(hipStreamSynchronize(d.stream));
+  return PV_OK;
+}
+
+int pv_tally_device(const uint32_t* verdict_bits, const uint32_t* dup_mask, uint64_t n_batches, uint32_t n_nodes,
+                    uint32_t quorum, uint8_t* reached, uint32_t* votes, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n_nodes == 0) return fail(PV_EINVAL, "n_nodes must be >= 1");
+  if (n_batches == 0) return PV_OK;
+  if (!verdict_bits || !reached) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(pv::launch_tally_bits(verdict_bits, dup_mask, n_batches, n_nodes, quorum, votes, reached, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_tally(const uint32_t* verdict_bits, const uint32_t* dup_mask, uint64_t n_batches, uint32_t n_nodes,
+             uint32_t quorum, uint8_t* reached) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (n_nodes == 0) return fail(PV_EINVAL, "n_nodes must be >= 1");
+  if (n_batches == 0) return PV_OK;
+  if (!verdict_bits || !reached) return fail(PV_EINVAL, "null buffer");
+  Device& d = g_devs[0];
+  HIP_OK(hipSetDevice(d.id));
+  const uint64_t words = n_batches * ((n_nodes + 31) / 32);
+  HIP_OK(d.tbits.ensure(2 * words));
+  HIP_OK(d.reached.ensure(n_batches));
+  HIP_OK(hipMemcpyAsync(d.tbits.p, verdict_bits, words * 4, hipMemcpyHostToDevice, d.stream));
+  if (dup_mask) HIP_OK(hipMemcpyAsync(d.tbits.p + words, dup_mask, words * 4, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(pv::launch_tally_bits(d.tbits.p, dup_mask ? d.tbits.p + words : nullptr, n_batches, n_nodes, quorum, nullptr,
+                               d.reached.p, d.stream));
   HIP_OK(hipMemcpyAsync(reached, d.reached.p, n_batches, hipMemcpyDeviceToHost, d.stream));
   HIP_OK(hipStreamSynchronize(d.stream));
   return PV_OK;

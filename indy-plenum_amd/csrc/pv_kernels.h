@@ -80,10 +80,13 @@ hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* 
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n,
                        const uint32_t* btab, uint8_t* pk_out, uint8_t* sig_out, hipStream_t s);
 
-// per-batch quorum tally over verdicts
+// per-batch quorum tally over per-message verdicts + sender indices (*bad |= 1
+// when a sender index is >= n_nodes), and over node-indexed voter bitmaps
 hipError_t launch_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off,
                         uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t* votes,
-                        uint8_t* reached, hipStream_t s);
+                        uint8_t* reached, uint32_t* bad, hipStream_t s);
+hipError_t launch_tally_bits(const uint32_t* bits, const uint32_t* dup, uint64_t n_batches, uint32_t n_nodes,
+                             uint32_t quorum, uint32_t* votes, uint8_t* reached, hipStream_t s);
 
 // SHA-256 / Merkle: out (n x 8 words) = SHA-256(prefix || M_i)
 // (plen 0 or 1 prefix bytes); one Merkle level m -> ceil(m/2) nodes

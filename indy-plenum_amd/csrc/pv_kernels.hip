@@ -360,22 +360,26 @@ hipError_t launch_sign(const uint8_t* seeds, const uint8_t* blob, const uint64_t
 
 // ------------------------------------------------------------------- tally
 // One wavefront per 3PC batch: lanes OR (1 << sender) of valid votes into the
-// voter set (duplicates collapse), popcount, compare with the quorum.
+// voter set (duplicates collapse), popcount, compare with the quorum.  A sender
+// index >= n_nodes is an argument error: it sets *bad (the API reports it)
+// instead of silently losing the vote.
 // plenum/server/models.py:24-45,91-114 ; plenum/server/quorums.py:15-39
 __global__ __launch_bounds__(256) void k_tally(const uint8_t* __restrict__ verdict, const uint32_t* __restrict__ sender,
                                                 const uint64_t* __restrict__ batch_off, uint64_t n_batches,
                                                 uint32_t n_nodes, uint32_t quorum, uint32_t* __restrict__ votes,
-                                                uint8_t* __restrict__ reached) {
+                                                uint8_t* __restrict__ reached, uint32_t* __restrict__ bad) {
   const uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (b >= n_batches) return;
   const uint64_t s0 = batch_off[b], s1 = batch_off[b + 1];
   const uint32_t words = (n_nodes + 63) / 64;  // voter-set words; n_nodes <= 1024 (16 words)
   uint32_t count = 0;
+  bool oob = false;
   for (uint32_t w = 0; w < words; ++w) {
     uint64_t mine = 0;
     for (uint64_t m = s0 + lane; m < s1; m += 64) {
       const uint32_t snd = sender[m];
+      oob = oob || snd >= n_nodes;
       if (verdict[m] && snd < n_nodes && (snd >> 6) == w) mine |= 1ull << (snd & 63);
     }
     // wave OR-reduction
@@ -387,6 +391,7 @@ __global__ __launch_bounds__(256) void k_tally(const uint8_t* __restrict__ verdi
     }
     count += __popcll(mine);
   }
+  if (__ballot(oob) && lane == 0) atomicOr(bad, 1u);
   if (lane == 0) {
     votes[b] = count;
     reached[b] = count >= quorum ? 1 : 0;
@@ -394,11 +399,43 @@ __global__ __launch_bounds__(256) void k_tally(const uint8_t* __restrict__ verdi
 }
 
 hipError_t launch_tally(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
-                        uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached, hipStream_t s) {
+                        uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached, uint32_t* bad,
+                        hipStream_t s) {
   if (n_batches == 0) return hipSuccess;
   const uint64_t blocks = (n_batches * 64 + 255) / 256;
   hipLaunchKernelGGL(k_tally, dim3((uint32_t)blocks), dim3(256), 0, s, verdict, sender, batch_off, n_batches, n_nodes,
-                     quorum, votes, reached);
+                     quorum, votes, reached, bad);
+  return hipGetLastError();
+}
+
+// SURVEY.md §8(b) bitmap form: batch b's voter set is already a bitmap
+// (bit j of word w = node 32 w + j has a valid vote), words_per = ceil(n_nodes/32)
+// words per batch; dup_mask (may be null) clears the nodes whose votes must
+// not count.  One lane per batch: popcount of (bits & ~dup) over the words,
+// bits >= n_nodes ignored.
+__global__ __launch_bounds__(256) void k_tally_bits(const uint32_t* __restrict__ bits, const uint32_t* __restrict__ dup,
+                                                     uint64_t n_batches, uint32_t n_nodes, uint32_t quorum,
+                                                     uint32_t* __restrict__ votes, uint8_t* __restrict__ reached) {
+  const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= n_batches) return;
+  const uint32_t wp = (n_nodes + 31) / 32;
+  uint32_t count = 0;
+  for (uint32_t w = 0; w < wp; ++w) {
+    uint32_t x = bits[b * wp + w];
+    if (dup) x &= ~dup[b * wp + w];
+    const uint32_t top = n_nodes - 32 * w;    // nodes in this word
+    if (top < 32) x &= (1u << top) - 1u;
+    count += __popc(x);
+  }
+  if (votes) votes[b] = count;
+  reached[b] = count >= quorum ? 1 : 0;
+}
+
+hipError_t launch_tally_bits(const uint32_t* bits, const uint32_t* dup, uint64_t n_batches, uint32_t n_nodes,
+                             uint32_t quorum, uint32_t* votes, uint8_t* reached, hipStream_t s) {
+  if (n_batches == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tally_bits, dim3((uint32_t)((n_batches + 255) / 256)), dim3(256), 0, s, bits, dup, n_batches,
+                     n_nodes, quorum, votes, reached);
   return hipGetLastError();
 }
 

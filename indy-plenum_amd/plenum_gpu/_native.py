@@ -27,8 +27,11 @@ SIGNATURES = [
     ('pv_device_count', ctypes.c_int, []),
     ('pv_verify_batch', ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, ctypes.c_uint32]),
     ('pv_verify_batch_device', ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
-    ('pv_tally', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ('pv_tally', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     ('pv_tally_device', ctypes.c_int,
+     [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_tally_votes', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ('pv_tally_votes_device', ctypes.c_int,
      [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_int, _vp]),
     ('pv_sign_batch', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     ('pv_sign_batch_device', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
@@ -229,9 +232,28 @@ def tally_arrays(verdict, sender, batch_off, n_nodes, quorum):
     reached = np.zeros(max(nb, 0), dtype=np.uint8)
     if nb <= 0:
         return votes, reached.astype(bool)
-    _check('pv_tally', load().pv_tally(_ptr(verdict), _ptr(sender), _ptr(batch_off), nb, n_nodes, quorum,
-                                        _ptr(votes), _ptr(reached)))
+    _check('pv_tally_votes', load().pv_tally_votes(_ptr(verdict), _ptr(sender), _ptr(batch_off), nb, n_nodes,
+                                                    quorum, _ptr(votes), _ptr(reached)))
     return votes, reached.astype(bool)
+
+
+def tally_bits_arrays(verdict_bits, n_nodes, quorum, dup_mask=None):
+    """pv_tally: verdict_bits / dup_mask (n_batches, ceil(n_nodes/32))
+    uint32 node-indexed voter bitmaps -> reached (n_batches,) bool."""
+    ensure_init()
+    w = (int(n_nodes) + 31) // 32
+    bits = np.ascontiguousarray(verdict_bits, dtype=np.uint32).reshape(-1, w)
+    nb = bits.shape[0]
+    dup = None
+    if dup_mask is not None:
+        dup = np.ascontiguousarray(dup_mask, dtype=np.uint32).reshape(-1, w)
+        if dup.shape != bits.shape:
+            raise ValueError('dup_mask shape {} != verdict_bits shape {}'.format(dup.shape, bits.shape))
+    reached = np.zeros(nb, dtype=np.uint8)
+    if nb:
+        _check('pv_tally', load().pv_tally(_ptr(bits), _ptr(dup) if dup is not None else None, nb, int(n_nodes),
+                                            int(quorum), _ptr(reached)))
+    return reached.astype(bool)
 
 
 def sign_batch_arrays(seeds, blob, off):

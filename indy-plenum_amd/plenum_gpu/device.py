@@ -150,7 +150,7 @@ def tally_device(verdict, sender, batch_off, n_nodes, quorum, votes, reached):
     dev = verdict.device
     nat.ensure_init(1 << dev.index)
     nb = batch_off.shape[0] - 1
-    nat._check('pv_tally_device',
-               nat.load().pv_tally_device(_p(verdict), _p(sender), _p(batch_off), nb, n_nodes, quorum, _p(votes),
-                                          _p(reached), dev.index, _stream(dev)))
+    nat._check('pv_tally_votes_device',
+               nat.load().pv_tally_votes_device(_p(verdict), _p(sender), _p(batch_off), nb, n_nodes, quorum,
+                                                _p(votes), _p(reached), dev.index, _stream(dev)))
     return votes, reached

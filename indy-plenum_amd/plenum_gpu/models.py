@@ -96,38 +96,92 @@ def tally_batches(verdict, sender, batch_off, n_nodes, quorum):
                                 np.asarray(batch_off, np.uint64), int(n_nodes), int(quorum))
 
 
-def propagate_quorums(req_keys, senders, verdict, n_nodes, node_index=None):
-    """PROPAGATE f+1 quorum per request (row f4): ReqState.req_with_acceptable_quorum
-    (plenum/server/propagator.py:36-44) over many requests at once with the same
-    GPU tally as COMMITs — one vote per distinct sender whose PROPAGATE carried a
-    valid request signature, reached iff votes >= Quorums(n).propagate (f + 1).
+PropagateQuorum = namedtuple('PropagateQuorum', ['votes', 'reached', 'finalised_by', 'event'])
 
-    req_keys (m,) request key of each PROPAGATE, senders (m,) node names (or
-    indices), verdict (m,) bool.  Returns {key: (votes, reached)} in first-seen order.
+
+def propagate_groups(req_keys, senders, verdict):
+    """Host half of `propagate_quorums`: the layout of the reference Requests
+    store (plenum/server/propagator.py:20-46, 111-134) after a stream of
+    PROPAGATEs, as tally input.
+
+    A PROPAGATE enters the store only when its request's signature verified
+    (Node.validateNodeMsg -> verifySignature, node.py:2624-2655): `verdict`
+    False drops it.  `Requests.add_propagate` keys the store by request key and
+    keeps ONE entry per sender (`propagates[sender] = req`: a re-sent PROPAGATE
+    replaces the copy, never adds a vote, and keeps the sender's first position).
+    `req_with_acceptable_quorum` counts only `str` senders (the reference's
+    workaround for byte-named senders); every other sender is stored but never
+    counted.  All copies under one key share one digest (key == digest,
+    request.py:82-84), so the count is the number of distinct str senders.
+
+    Returns (order, batch_off, sender_idx, counts, names, first): `order` the
+    keys in the order their first accepted PROPAGATE arrived; batch j =
+    [batch_off[j], batch_off[j+1]) of the flat (sender_idx, counts) arrays, one
+    entry per (key, sender) in first-arrival order (counts 0 for non-str
+    senders); names[i] the str sender of index i; first[k] the last accepted
+    event index of flat entry k (the copy the store holds).
+    """
+    names, index = [], {}
+    groups = {}            # key -> {sender: flat position} (dict: insertion order)
+    latest = {}            # (key, sender) -> last accepted event index
+    for ev, (key, snd, ok) in enumerate(zip(req_keys, senders, verdict)):
+        if not ok:
+            continue
+        g = groups.setdefault(key, {})
+        g.setdefault(snd, None)
+        latest[(key, snd)] = ev
+    order = list(groups)
+    off = [0]
+    sender_idx, counts, last = [], [], []
+    for key in order:
+        for snd in groups[key]:
+            counted = isinstance(snd, str)
+            if counted and snd not in index:
+                index[snd] = len(names)
+                names.append(snd)
+            sender_idx.append(index[snd] if counted else 0)
+            counts.append(1 if counted else 0)
+            last.append(latest[(key, snd)])
+        off.append(len(sender_idx))
+    return (order, np.asarray(off, np.uint64), np.asarray(sender_idx, np.uint32), np.asarray(counts, np.uint8),
+            names, np.asarray(last, np.int64))
+
+
+def propagate_quorums(req_keys, senders, verdict, n_nodes):
+    """PROPAGATE f+1 quorum per request (row f4) for a whole stream of
+    PROPAGATEs at once: `Requests.add_propagate` for every PROPAGATE whose
+    request signature verified, then `req_with_acceptable_quorum(
+    Quorums(n_nodes).propagate)` per request (plenum/server/propagator.py:38-46,
+    111-134), with the voter sets counted by the GPU tally (k_tally).
+
+    req_keys (m,) request key of each PROPAGATE in arrival order, senders (m,)
+    sender names (non-str names are stored but never counted, as in the
+    reference), verdict (m,) bool signature verdicts.  Returns
+    {key: PropagateQuorum(votes, reached, finalised_by, event)} in the store's
+    order: votes = distinct str senders, reached = votes >= f + 1,
+    finalised_by = the str sender whose copy req_with_acceptable_quorum returns
+    (the (f+1)-th distinct str sender in arrival order; None if not reached),
+    event = index of that copy's PROPAGATE in the stream.
     """
     from .quorums import Quorums
-    order, groups = [], {}
-    for k, key in enumerate(req_keys):
-        if key not in groups:
-            groups[key] = []
-            order.append(key)
-        groups[key].append(k)
-    names = dict(node_index or {})
-    idx = []
-    for s in senders:
-        if isinstance(s, (int, np.integer)):
-            idx.append(int(s))
-        else:
-            if s not in names:
-                names[s] = len(names)
-            idx.append(names[s])
-    flat, off = [], [0]
-    for key in order:
-        flat.extend(groups[key])
-        off.append(len(flat))
-    flat = np.asarray(flat, np.int64)
-    sender = np.asarray(idx, np.uint32)[flat] if len(flat) else np.zeros(0, np.uint32)
-    ver = np.asarray(verdict, bool)[flat] if len(flat) else np.zeros(0, bool)
-    votes, reached = tally_batches(ver, sender, np.asarray(off, np.uint64), max(n_nodes, len(names)),
-                                   Quorums(n_nodes).propagate.value)
-    return {key: (int(votes[j]), bool(reached[j])) for j, key in enumerate(order)}
+    if not (len(req_keys) == len(senders) == len(verdict)):
+        raise ValueError('req_keys, senders and verdict must have one entry per PROPAGATE')
+    order, off, sender_idx, counts, names, last = propagate_groups(req_keys, senders, verdict)
+    q = Quorums(n_nodes).propagate.value
+    if not order:
+        return {}
+    if len(names) > 1024:
+        raise ValueError('at most 1024 distinct senders per stream (got {})'.format(len(names)))
+    votes, reached = tally_batches(counts, sender_idx, off, max(1, len(names)), q)
+    out = {}
+    for j, key in enumerate(order):
+        by, ev = None, None
+        if reached[j]:
+            seen = 0
+            for k in range(int(off[j]), int(off[j + 1])):
+                seen += int(counts[k])
+                if seen == q:
+                    by, ev = names[int(sender_idx[k])], int(last[k])
+                    break
+        out[key] = PropagateQuorum(int(votes[j]), bool(reached[j]), by, ev)
+    return out

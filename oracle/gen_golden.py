@@ -29,6 +29,13 @@ Fixtures
   merkle.json           Merkle Tree Hash roots (ledger/tree_hasher.py TreeHasher.hash_full_tree,
                         checked against CompactMerkleTree.extend) over leaves of every length
                         around the SHA-256 block boundaries, leaf and child hashes
+  propagate.json        PROPAGATE f+1 quorums (row f4): streams of PROPAGATEs (re-sent,
+                        duplicate and non-str senders, tampered and re-signed requests)
+                        through the reference Requests.add_propagate /
+                        req_with_acceptable_quorum (plenum/server/propagator.py:20-46,
+                        111-134) with Quorums(n).propagate; a PROPAGATE reaches
+                        add_propagate only if ReqAuthenticator.authenticate accepts its
+                        request (Node.validateNodeMsg -> verifySignature, node.py:2624-2655)
   ingress.json          one node service pass for the batched-ingestion path (f1):
                         client requests of every shape with the reference
                         Request(**req).key (plenum/common/request.py:82-120) and the
@@ -702,6 +709,89 @@ def gen_ingress(n=48):
     return {'registry': registry, 'write_types': ['buy'], 'cases': cases, 'propagates': props, 'batches': batches}
 
 
+def gen_propagate():
+    """PROPAGATE streams through the reference Requests store.  Per stream:
+    events [sender, case index] in arrival order (sender a node name, or a
+    bytes name — the non-str sender the reference filters out), the
+    per-request outcome: Requests.votes (every sender), the str-sender count
+    and whether req_with_acceptable_quorum(Quorums(n).propagate) returns a
+    request (and which sender's copy)."""
+    from plenum.common.request import Request
+    from plenum.server.propagator import Requests
+    rnd = random.Random(777)
+    n_clients = 40
+    signers = [DidSigner(seed=det_seed(b'plenum-gpu/propagate', i)) for i in range(n_clients)]
+    authnr = CoreAuthNr(['buy'], [], [])
+    registry = {}
+    for sg in signers:
+        authnr.addIdr(sg.identifier, sg.verkey)
+        registry[sg.identifier] = sg.verkey
+    ra = ReqAuthenticator()
+    ra.register_authenticator(authnr)
+    cases = []
+    for i in range(n_clients):
+        sg = signers[i]
+        req = {'identifier': sg.identifier, 'reqId': 7000 + i,
+               'operation': {'type': 'buy', 'data': payload_chars(12000 + i, 24 + i % 17)}, 'protocolVersion': 2}
+        req['signature'] = sg.sign(req)
+        kind = 'valid'
+        if i % 5 == 3:      # tampered in transit: the signature no longer verifies
+            req['operation']['data'] += 'x'
+            kind = 'tampered'
+        cases.append({'kind': kind, 'req': req})
+        if i % 7 == 2:      # the client re-signs a second operation under the same reqId
+            req2 = {'identifier': sg.identifier, 'reqId': 7000 + i,
+                    'operation': {'type': 'buy', 'data': payload_chars(13000 + i, 30)}, 'protocolVersion': 2}
+            req2['signature'] = sg.sign(req2)
+            cases.append({'kind': 'resigned', 'req': req2})
+    for c in cases:
+        c['key'] = Request(**c['req']).key
+        try:
+            ra.authenticate(json.loads(json.dumps(c['req'])))
+            c['valid'] = True
+        except Exception:
+            c['valid'] = False
+    streams = []
+    for n in (4, 7, 25):
+        quorums = Quorums(n)
+        names = ['Node%d' % (j + 1) for j in range(n)]
+        events = []
+        for ci in range(len(cases)):
+            # how many distinct nodes propagate this request: around the f+1 boundary
+            k = max(0, min(n, quorums.propagate.value + rnd.choice([-2, -1, -1, 0, 0, 1, 3])))
+            for j in rnd.sample(range(n), k):
+                events.append([names[j], ci])
+            if rnd.random() < 0.3:          # a node re-sends its PROPAGATE
+                events.append([names[rnd.randrange(n)], ci])
+            if rnd.random() < 0.2:          # a non-str (bytes) sender name
+                events.append([{'bytes': names[rnd.randrange(n)]}, ci])
+        rnd.shuffle(events)
+        store = Requests()
+        order = []
+        for snd, ci in events:
+            c = cases[ci]
+            if not c['valid']:
+                continue                     # verifySignature rejected the PROPAGATE
+            sender = snd['bytes'].encode() if isinstance(snd, dict) else snd
+            req = Request(**json.loads(json.dumps(c['req'])))
+            if req.key not in store:
+                order.append(req.key)
+            store.add_propagate(req, sender)
+        outcome = {}
+        for key in order:
+            state = store[key]
+            got = state.req_with_acceptable_quorum(quorums.propagate)
+            str_senders = [s for s in state.propagates if isinstance(s, str)]
+            outcome[key] = {'votes': store.votes(state.request), 'str_votes': len(str_senders),
+                            'reached': got is not None,
+                            'finalised_by': (str_senders[quorums.propagate.value - 1] if got is not None else None)}
+            if got is not None:
+                assert got is state.propagates[outcome[key]['finalised_by']]
+        streams.append({'n': n, 'f': quorums.f, 'quorum': quorums.propagate.value, 'events': events,
+                        'order': order, 'outcome': outcome})
+    return {'registry': registry, 'write_types': ['buy'], 'cases': cases, 'streams': streams}
+
+
 def gen_merkle():
     """Merkle Tree Hash roots from the reference ledger/tree_hasher.py TreeHasher
     (and CompactMerkleTree for the incremental form) over deterministic leaves of
@@ -724,7 +814,7 @@ def gen_merkle():
                          for i in range(0, 20, 2)]}
 
 
-GENERATORS = ['kat', 'plenum_requests', 'raw_vectors', 'adversarial', 'tally', 'ingress', 'merkle']
+GENERATORS = ['kat', 'plenum_requests', 'raw_vectors', 'adversarial', 'tally', 'ingress', 'merkle', 'propagate']
 
 
 def main(which=None):
@@ -745,6 +835,9 @@ def main(which=None):
     if 'merkle' in which:
         with open(os.path.join(OUT, 'merkle.json'), 'w') as fh:
             json.dump(gen_merkle(), fh, indent=0)
+    if 'propagate' in which:
+        with open(os.path.join(OUT, 'propagate.json'), 'w') as fh:
+            json.dump(gen_propagate(), fh, indent=0)
     if 'ingress' in which:
         with open(os.path.join(OUT, 'ingress.json'), 'w') as fh:
             json.dump(gen_ingress(), fh, indent=0)

@@ -202,3 +202,41 @@ def test_c4_shape_properties(torch_dev):
     tamper = b.tamper.cpu().numpy().astype(bool)
     assert (v == ~tamper).all()
     assert 0.045 < tamper.mean() < 0.055
+
+
+def test_c4_full_shard(torch_dev):
+    """BASELINE configs[3] as configured, per GPU: the full 8M-signature shard of
+    the 64M / 8-GPU batch (payloads uniform 128 B..4 KB, key pool 2^20, ~5 %
+    tampered), through the unkeyed path and the prepared-key path.  Size-
+    independent properties on all 8M (verdict == not tampered, bitmap ==
+    verdicts, both paths identical) and a 2048-signature oracle spot check
+    spread over the shard."""
+    import torch
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch
+    n = 8_000_000
+    b = SyntheticBatch(0, n, 128, cfg=4, first=3 * n, key_mod=1 << 20, mode=synth.RANGE, mlen_max=4096)
+    tamper = b.tamper.cpu().numpy().astype(bool)
+    assert 0.049 < tamper.mean() < 0.051
+    verdicts = []
+    for keyed in (False, True):
+        assert b.use_key_cache(keyed) == keyed
+        b.bitmap.zero_()
+        v = b.verify().cpu().numpy().astype(bool)
+        bits = np.unpackbits(b.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
+        assert (bits == v).all()
+        assert (v == ~tamper).all()
+        verdicts.append(v)
+    assert (verdicts[0] == verdicts[1]).all()
+    rng = np.random.default_rng(44)
+    idx = np.sort(rng.choice(n, 2048, replace=False))
+    it = torch.from_numpy(idx).to(b.pk.device)
+    pk = b.pk[it].cpu().numpy()
+    sig = b.sig[it].cpu().numpy()
+    off = b.off.cpu().numpy()
+    msgs = [b.blob[int(off[i]):int(off[i + 1])].cpu().numpy() for i in idx]
+    loff = np.zeros(len(idx) + 1, np.uint64)
+    loff[1:] = np.cumsum([len(m) for m in msgs])
+    want = orc.verify_batch(pk, sig, np.concatenate(msgs), loff)
+    assert (verdicts[0][idx] == want).all()
+    assert not want.all() and want.any()
