@@ -347,6 +347,48 @@ def main_f3(args):
             nx.append(lv[-1])
         lv = nx
     mism += int(ext_root != lv[0]) + int(len(ext_hashes) != bin(n - 1).count('1'))
+    # CompactMerkleTree.append x 10k (ledger/compact_merkle_tree.py:155-160): per
+    # leaf _hash_full(leaves, 0, 1) + one hash_children per carry, then the root
+    # fold — the call pattern of the reference tree driven by GpuTreeHasher
+    # (single hashes stay on hashlib: no GPU call per node)
+    n_app = min(10_000, n - 1)
+
+    def appends(hasher):
+        size, hashes = 0, []
+        for i in range(n_app):
+            h, _ = hasher._hash_full(host_leaves, i, i + 1)
+            s = size
+            while s & 1:            # carries: merge equal-size subtrees
+                h = hasher.hash_children(hashes.pop(), h)
+                s >>= 1
+            hashes.append(h)
+            size += 1
+        return hasher._hash_fold(tuple(hashes))
+    t0 = time.perf_counter()
+    app_root = appends(th)
+    app_s = time.perf_counter() - t0
+    lv = leaf_hashes[:n_app]
+    while len(lv) > 1:
+        nx = [hashlib.sha256(b'\x01' + lv[i] + lv[i + 1]).digest() for i in range(0, len(lv) - 1, 2)]
+        if len(lv) % 2:
+            nx.append(lv[-1])
+        lv = nx
+    mism += int(app_root != lv[0])
+    # small batches: sha256_batch / merkle_root around the host/GPU dispatch size
+    from plenum_gpu import merkle as mk_mod
+    small = []
+    for k in (64, 256, 1024, 4096, 16384):
+        msgs = host_leaves[:k]
+        row = {'items': k}
+        for tag, thr in (('host', 1 << 62), ('gpu', 0)):
+            mk_mod.GPU_MIN_ITEMS = thr
+            mk_mod.sha256_batch(msgs, prefix=0)
+            t0 = time.perf_counter()
+            for _ in range(5):
+                mk_mod.sha256_batch(msgs, prefix=0)
+            row[tag + '_us'] = round((time.perf_counter() - t0) / 5 * 1e6, 1)
+        small.append(row)
+    mk_mod.GPU_MIN_ITEMS = 512
     value = n * args.steps / elapsed
     res = {
         'metric': 'Merkle tree hash leaves/sec (ledger TreeHasher.hash_full_tree, SHA-256)', 'value': round(value, 1),
@@ -361,6 +403,13 @@ def main_f3(args):
                            'path': 'GpuTreeHasher._hash_full over {} host leaves (list of bytes packed once; {} full subtrees, '
                                    'one pv_merkle_root call each incl. H2D), root checked against '
                                    'hashlib'.format(n - 1, bin(n - 1).count('1'))},
+        'compact_append': {'value': round(n_app / app_s, 1), 'unit': 'appends/s', 'appends': n_app,
+                           'ms': round(app_s * 1e3, 3),
+                           'path': 'CompactMerkleTree.append call pattern (_hash_full of 1 leaf + hash_children per '
+                                   'carry + _hash_fold) on GpuTreeHasher; root checked against hashlib'},
+        'sha256_batch_small': {'rows': small, 'dispatch_items': 512,
+                               'path': 'sha256_batch(host list of 256 B leaves, prefix 0x00): hashlib vs one GPU '
+                                       'call incl. pack + H2D + D2H, mean of 5'},
         'roofline': None,
         'cpu_baseline': {'value': round(cpu_rate, 1), 'unit': 'leaves/s', 'cores': 1, 'kind': 'port',
                          'sample': 'hashlib SHA-256 tree hash (the reference TreeHasher algorithm, level-wise) over '

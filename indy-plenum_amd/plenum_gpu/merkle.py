@@ -10,13 +10,52 @@
   bulk step) computed on the GPU (pv_merkle_root): leaf = SHA-256(0x00 || data),
   node = SHA-256(0x01 || left || right), RFC 6962 shape.
 
-Like the verify path there is no CPU fallback: the library and a GPU are required.
+Size dispatch (not a fallback): one GPU call costs tens to hundreds of
+microseconds of launch + PCIe round trip, one SHA-256 of a leaf or an inner
+node costs ~0.5 µs in hashlib.  So single hashes (`hash_leaf`,
+`hash_children`, `_hash_fold`, `hash_empty` — what `CompactMerkleTree.append`
+and its carry chain call per leaf, ledger/compact_merkle_tree.py:138-160) and
+batches / subtrees below `GPU_MIN_ITEMS` items are hashed on the host with
+hashlib, exactly as the reference TreeHasher does (ledger/tree_hasher.py:4,
+21-28); larger batches and subtrees go to the GPU, which is required for them
+(no CPU fallback there: a missing library or GPU raises).
 """
 import ctypes
+import hashlib
 
 import numpy as np
 
 from . import _native as nat
+
+# batches / (sub)trees with fewer items than this are hashed on the host
+# (profiles/r02_f3_small.jsonl: hashlib and one GPU call break even near
+# 256 leaves of 256 B; the GPU is 2x faster at 1024); tests set it to 0 to
+# push every size through the GPU kernels
+GPU_MIN_ITEMS = 512
+
+
+def _leaf(d):
+    return hashlib.sha256(b'\x00' + bytes(d)).digest()
+
+
+def _node(left, right):
+    return hashlib.sha256(b'\x01' + bytes(left) + bytes(right)).digest()
+
+
+def _host_mth(leaves):
+    """RFC 6962 Merkle Tree Hash, level-wise (an odd last node moves up: the
+    same shape as ledger/tree_hasher.py:45-62's split at the largest power of
+    two below n)."""
+    if not leaves:
+        return hashlib.sha256(b'').digest(), []
+    lh = [_leaf(d) for d in leaves]
+    lvl = lh
+    while len(lvl) > 1:
+        nxt = [_node(lvl[i], lvl[i + 1]) for i in range(0, len(lvl) - 1, 2)]
+        if len(lvl) & 1:
+            nxt.append(lvl[-1])
+        lvl = nxt
+    return lvl[0], lh
 
 
 def _pack(msgs):
@@ -27,10 +66,13 @@ def _pack(msgs):
 
 def sha256_batch(msgs, prefix=None):
     """[bytes] -> [32-byte digest of (prefix || m)]; prefix None or a byte value."""
-    nat.ensure_init()
     n = len(msgs)
     if n == 0:
         return []
+    if n < GPU_MIN_ITEMS:
+        pre = b'' if prefix is None else bytes([int(prefix)])
+        return [hashlib.sha256(pre + bytes(m)).digest() for m in msgs]
+    nat.ensure_init()
     blob, off = _pack(msgs)
     out = np.zeros((n, 32), np.uint8)
     p = -1 if prefix is None else int(prefix)
@@ -47,8 +89,11 @@ def request_digests(reqs, plugin_fields=()):
 
 def merkle_root(leaves, with_leaf_hashes=False):
     """RFC 6962 Merkle Tree Hash of `leaves` (bytes each) on the GPU."""
-    nat.ensure_init()
     n = len(leaves)
+    if n < GPU_MIN_ITEMS:
+        root, lh = _host_mth(leaves)
+        return (root, lh) if with_leaf_hashes else root
+    nat.ensure_init()
     blob, off = _pack(leaves)
     root = np.zeros(32, np.uint8)
     lh = np.zeros((max(n, 1), 32), np.uint8) if with_leaf_hashes else None
@@ -66,16 +111,16 @@ class GpuTreeHasher:
         return 'GpuTreeHasher()'
 
     def hash_empty(self):
-        return merkle_root([])
+        return hashlib.sha256(b'').digest()
 
     def hash_leaf(self, data):
-        return sha256_batch([data], prefix=0x00)[0]
+        return _leaf(data)
 
     def hash_leaves(self, leaves):
         return sha256_batch(leaves, prefix=0x00)
 
     def hash_children(self, left, right):
-        return sha256_batch([bytes(left) + bytes(right)], prefix=0x01)[0]
+        return _node(left, right)
 
     def hash_full_tree(self, leaves):
         return merkle_root(leaves)
@@ -94,15 +139,21 @@ class GpuTreeHasher:
         width = r_idx - l_idx
         if width == 0:
             return self.hash_empty(), ()
-        nat.ensure_init()
-        blob, off = _pack(leaves[l_idx:r_idx])   # packed once; each subtree is an offset window
-        lib, hashes, a = nat.load(), [], 0
+        hashes, a = [], 0
+        big = width >= GPU_MIN_ITEMS
+        if big:
+            nat.ensure_init()
+            blob, off = _pack(leaves[l_idx:r_idx])   # packed once; each subtree is an offset window
+            lib = nat.load()
         for bit in range(width.bit_length() - 1, -1, -1):
             if width >> bit & 1:
-                root = np.zeros(32, np.uint8)
-                nat._check('pv_merkle_root', lib.pv_merkle_root(nat._ptr(blob), nat._ptr(off[a:]), 1 << bit,
-                                                                nat._ptr(root), ctypes.c_void_p(0)))
-                hashes.append(root.tobytes())
+                if (1 << bit) < GPU_MIN_ITEMS:
+                    hashes.append(_host_mth(leaves[l_idx + a:l_idx + a + (1 << bit)])[0])
+                else:
+                    root = np.zeros(32, np.uint8)
+                    nat._check('pv_merkle_root', lib.pv_merkle_root(nat._ptr(blob), nat._ptr(off[a:]), 1 << bit,
+                                                                    nat._ptr(root), ctypes.c_void_p(0)))
+                    hashes.append(root.tobytes())
                 a += 1 << bit
         hashes = tuple(hashes)
         if len(hashes) == 1:

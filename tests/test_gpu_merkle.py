@@ -11,6 +11,16 @@ import _merkle as mk
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=['all_gpu', 'dispatch'])
+def gpu_min(request, monkeypatch):
+    """'all_gpu': every batch / subtree through the GPU kernels (GPU_MIN_ITEMS = 0);
+    'dispatch': the production size dispatch (small ones on hashlib)."""
+    from plenum_gpu import merkle
+    if request.param == 'all_gpu':
+        monkeypatch.setattr(merkle, 'GPU_MIN_ITEMS', 0)
+    return request.param
+
+
 def test_sha256_batch_vs_hashlib():
     from plenum_gpu.merkle import sha256_batch
     rng = np.random.default_rng(9)

@@ -66,3 +66,39 @@ def test_compact_tree_restatement_vs_reference_states():
         assert tree.size == st['tree_size'] == pos
         assert [h.hex() for h in tree.hashes] == st['hashes']
         assert tree.root().hex() == st['root'] == mk.mth_levelwise(leaves[:pos]).hex()
+
+
+def test_small_work_never_touches_the_library(monkeypatch):
+    """single hashes and small batches (CompactMerkleTree.append's
+    hash_leaf + carry chain of hash_children, ledger/compact_merkle_tree.py:138-160)
+    run on hashlib as the reference TreeHasher does — no GPU call per node — and
+    match the reference fixtures."""
+    from plenum_gpu import _native, merkle
+    from plenum_gpu.merkle import GpuTreeHasher, merkle_root, sha256_batch
+
+    def boom(*a, **k):
+        raise AssertionError('GPU library used for a small batch')
+    monkeypatch.setattr(_native, 'load', boom)
+    monkeypatch.setattr(_native, 'ensure_init', boom)
+    fx = mk.fixture()
+    th = GpuTreeHasher()
+    for t in fx['trees']:
+        if t['size'] < merkle.GPU_MIN_ITEMS:
+            assert th.hash_full_tree(fx['leaves'][:t['size']]).hex() == t['root']
+    root, lh = merkle_root(fx['leaves'][:70], with_leaf_hashes=True)
+    assert [h.hex() for h in lh] == fx['leaf_hashes']
+    assert sha256_batch([b'abc'], prefix=None) == [hashlib.sha256(b'abc').digest()]
+    tree = mk.CompactTree(th)
+    pos = 0
+    leaves = fx['leaves']
+    for st in mk.compact_fixture():
+        k = st['extend']
+        if pos + k >= merkle.GPU_MIN_ITEMS:
+            break
+        tree.extend(leaves[pos:pos + k])
+        pos += k
+        assert tree.size == st['tree_size'] and [h.hex() for h in tree.hashes] == st['hashes']
+        assert tree.root().hex() == st['root']
+    for i in range(pos, pos + 50):        # append = extend by one leaf
+        tree.extend([leaves[i % len(leaves)]])
+    assert tree.size == pos + 50
