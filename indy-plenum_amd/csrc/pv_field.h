@@ -36,12 +36,14 @@
 #ifndef PV_CHECK_SQ
 #define PV_CHECK_SQ(f)
 #endif
-// Keeps the scheduler from interleaving consecutive field multiplies: each
-// one has 10 independent accumulator chains (enough ILP), and interleaving
-// several multiplies multiplies the live 64-bit accumulators (register
-// pressure -> occupancy).  Device-only builtin; empty in host builds.
+// Optional scheduling fence after every field multiply (-DPV_FE_FENCE_ON):
+// keeps the scheduler from interleaving consecutive multiplies.  Off by
+// default since the column-asm multiply (below): with each column one asm
+// block the interleaving is limited anyway, and the fence-free build measured
+// equal on C2 and 1-3 % faster on the keyed C3 curve
+// (profiles/r02_ab_colasm_c2.json, r02_ab_colasm_c3.json).
 #ifndef PV_FE_FENCE
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PV_FE_FENCE_ON)
 #define PV_FE_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define PV_FE_FENCE()
@@ -58,6 +60,133 @@ struct fe {
 };
 
 PV_HD uint64_t mul32x32(uint32_t a, uint32_t b) { return (uint64_t)a * (uint64_t)b; }
+
+// Column sums as v_mad_u64_u32 chains whose first addend is the incoming
+// carry.  As plain C++ the compiler reassociates every column (starts it from
+// 0 and adds the carry with a trailing v_lshl_add_u64: one extra half-rate
+// 64-bit op per column, 10 per multiply).  A whole column is ONE asm block:
+// an asm statement cannot be reassociated, and the gfx950 hazard recognizer,
+// which assumes an inline-asm result feeding another inline asm needs a wait
+// state (dst-sel forwarding), then sees one asm block per column instead of
+// one per product (a per-product asm statement cost an s_nop 0 per MAD).
+// Dependent v_mad_u64_u32 need no wait states between them (the compiler's
+// own chains are back to back).  Host builds (tools/hostcheck) and
+// -DPV_FE_NOASM use the plain expressions: the same sums.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PV_FE_NOASM)
+#define PV_ASM_FN __device__ __forceinline__
+PV_ASM_FN uint64_t mad10(uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4, uint32_t a5, uint32_t b5, uint32_t a6, uint32_t b6, uint32_t a7, uint32_t b7, uint32_t a8, uint32_t b8, uint32_t a9, uint32_t b9) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0\n"
+      "v_mad_u64_u32 %0, vcc, %3, %4, %0\n"
+      "v_mad_u64_u32 %0, vcc, %5, %6, %0\n"
+      "v_mad_u64_u32 %0, vcc, %7, %8, %0\n"
+      "v_mad_u64_u32 %0, vcc, %9, %10, %0\n"
+      "v_mad_u64_u32 %0, vcc, %11, %12, %0\n"
+      "v_mad_u64_u32 %0, vcc, %13, %14, %0\n"
+      "v_mad_u64_u32 %0, vcc, %15, %16, %0\n"
+      "v_mad_u64_u32 %0, vcc, %17, %18, %0\n"
+      "v_mad_u64_u32 %0, vcc, %19, %20, %0\n"
+      : "=v"(d)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4), "v"(a5), "v"(b5), "v"(a6), "v"(b6), "v"(a7), "v"(b7), "v"(a8), "v"(b8), "v"(a9), "v"(b9), "0"(c)
+      : "vcc");
+  return d;
+}
+PV_ASM_FN uint64_t mad10z(uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4, uint32_t a5, uint32_t b5, uint32_t a6, uint32_t b6, uint32_t a7, uint32_t b7, uint32_t a8, uint32_t b8, uint32_t a9, uint32_t b9) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0\n"
+      "v_mad_u64_u32 %0, vcc, %3, %4, %0\n"
+      "v_mad_u64_u32 %0, vcc, %5, %6, %0\n"
+      "v_mad_u64_u32 %0, vcc, %7, %8, %0\n"
+      "v_mad_u64_u32 %0, vcc, %9, %10, %0\n"
+      "v_mad_u64_u32 %0, vcc, %11, %12, %0\n"
+      "v_mad_u64_u32 %0, vcc, %13, %14, %0\n"
+      "v_mad_u64_u32 %0, vcc, %15, %16, %0\n"
+      "v_mad_u64_u32 %0, vcc, %17, %18, %0\n"
+      "v_mad_u64_u32 %0, vcc, %19, %20, %0\n"
+      : "=&v"(d)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4), "v"(a5), "v"(b5), "v"(a6), "v"(b6), "v"(a7), "v"(b7), "v"(a8), "v"(b8), "v"(a9), "v"(b9)
+      : "vcc");
+  return d;
+}
+PV_ASM_FN uint64_t mad6(uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4, uint32_t a5, uint32_t b5) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0\n"
+      "v_mad_u64_u32 %0, vcc, %3, %4, %0\n"
+      "v_mad_u64_u32 %0, vcc, %5, %6, %0\n"
+      "v_mad_u64_u32 %0, vcc, %7, %8, %0\n"
+      "v_mad_u64_u32 %0, vcc, %9, %10, %0\n"
+      "v_mad_u64_u32 %0, vcc, %11, %12, %0\n"
+      : "=v"(d)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4), "v"(a5), "v"(b5), "0"(c)
+      : "vcc");
+  return d;
+}
+PV_ASM_FN uint64_t mad6z(uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4, uint32_t a5, uint32_t b5) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0\n"
+      "v_mad_u64_u32 %0, vcc, %3, %4, %0\n"
+      "v_mad_u64_u32 %0, vcc, %5, %6, %0\n"
+      "v_mad_u64_u32 %0, vcc, %7, %8, %0\n"
+      "v_mad_u64_u32 %0, vcc, %9, %10, %0\n"
+      "v_mad_u64_u32 %0, vcc, %11, %12, %0\n"
+      : "=&v"(d)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4), "v"(a5), "v"(b5)
+      : "vcc");
+  return d;
+}
+PV_ASM_FN uint64_t mad5(uint64_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0\n"
+      "v_mad_u64_u32 %0, vcc, %3, %4, %0\n"
+      "v_mad_u64_u32 %0, vcc, %5, %6, %0\n"
+      "v_mad_u64_u32 %0, vcc, %7, %8, %0\n"
+      "v_mad_u64_u32 %0, vcc, %9, %10, %0\n"
+      : "=v"(d)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4), "0"(c)
+      : "vcc");
+  return d;
+}
+PV_ASM_FN uint64_t mad5z(uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0\n"
+      "v_mad_u64_u32 %0, vcc, %3, %4, %0\n"
+      "v_mad_u64_u32 %0, vcc, %5, %6, %0\n"
+      "v_mad_u64_u32 %0, vcc, %7, %8, %0\n"
+      "v_mad_u64_u32 %0, vcc, %9, %10, %0\n"
+      : "=&v"(d)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4)
+      : "vcc");
+  return d;
+}
+#undef PV_ASM_FN
+#else
+#define PV_MADN_PLAIN 1
+#endif
+
+// column of n products a[0]b[0] + ... + a[n-1]b[n-1] (+ carry unless first)
+template <int N>
+PV_HD uint64_t column(const uint32_t a[N], const uint32_t b[N], uint64_t carry, bool first) {
+#if defined(PV_MADN_PLAIN)
+  uint64_t acc = first ? 0 : carry;
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc += mul32x32(a[i], b[i]);
+  return acc;
+#else
+  if constexpr (N == 10) {
+    if (first) return mad10z(a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3], a[4], b[4], a[5], b[5], a[6], b[6], a[7],
+                             b[7], a[8], b[8], a[9], b[9]);
+    return mad10(carry, a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3], a[4], b[4], a[5], b[5], a[6], b[6], a[7], b[7],
+                 a[8], b[8], a[9], b[9]);
+  } else if constexpr (N == 6) {
+    if (first) return mad6z(a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3], a[4], b[4], a[5], b[5]);
+    return mad6(carry, a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3], a[4], b[4], a[5], b[5]);
+  } else {
+    static_assert(N == 5, "column widths of fe_mul / fe_sq");
+    if (first) return mad5z(a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3], a[4], b[4]);
+    return mad5(carry, a[0], b[0], a[1], b[1], a[2], b[2], a[3], b[3], a[4], b[4]);
+  }
+#endif
+}
 
 PV_HD void fe_0(fe& h) {
 #pragma unroll
@@ -121,13 +250,15 @@ PV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   uint32_t out[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
-    uint64_t acc = carry;
+    uint32_t a[10], b[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
       const int j = (k - i + 10) % 10;
       const bool oo = (i & 1) && (j & 1);
-      acc += mul32x32(oo ? f2[i] : f.v[i], i + j >= 10 ? g19[j] : g.v[j]);
+      a[i] = oo ? f2[i] : f.v[i];
+      b[i] = i + j >= 10 ? g19[j] : g.v[j];
     }
+    const uint64_t acc = column<10>(a, b, carry, k == 0);
     carry = acc >> ((k & 1) ? 25 : 26);
     out[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
   }
@@ -150,7 +281,8 @@ PV_HD void fe_sq(fe& h, const fe& f) {
   uint32_t out[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
-    uint64_t acc = carry;
+    uint32_t as[6], bs[6];
+    int t = 0;
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
 #pragma unroll
@@ -168,9 +300,13 @@ PV_HD void fe_sq(fe& h, const fe& f) {
           a = oo ? f4[i] : f2[i];
           b = wrap ? f19[j] : f.v[j];
         }
-        acc += mul32x32(a, b);
+        as[t] = a;
+        bs[t] = b;
+        ++t;
       }
     }
+    // column k has 6 products when k is even, 5 when odd
+    const uint64_t acc = (k & 1) ? column<5>(as, bs, carry, false) : column<6>(as, bs, carry, k == 0);
     carry = acc >> ((k & 1) ? 25 : 26);
     out[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
   }
