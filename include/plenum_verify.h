@@ -95,9 +95,12 @@ int pv_device_count(void);
  *   msg_blob, msg_off  messages (see conventions)
  *   verdict n bytes out, 1 = valid, 0 = invalid
  * The batch is split into contiguous shards over the devices in device_mask
- * (0 = every initialised device); each shard runs as a pipeline of up to 8
- * chunks (H2D of chunk c+1 on a copy stream overlaps the kernels of chunk c).
- * Synchronous: returns after every verdict is in `verdict`. */
+ * (0 = every initialised device), each driven by its own host thread; a shard
+ * runs as a pipeline of about 8 chunks: host threads gather chunk c into a
+ * page-locked slot, its H2D runs on a copy stream, and its kernels run on one
+ * of two compute streams (chunk c+1's grid fills chunk c's tail).  msg_off must
+ * be non-decreasing (checked chunk by chunk before any kernel reads it:
+ * PV_EINVAL).  Synchronous: returns after every verdict is in `verdict`. */
 int pv_verify_batch(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
                     uint64_t n, uint8_t *verdict, uint32_t device_mask, uint32_t flags);
 
@@ -254,7 +257,7 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
 /* Host-side staging of pv_verify_batch's inputs, chosen by PV_HOST_STAGING /
  * PV_HOST_COPY_THREADS / PV_HOST_CHUNKS at pv_init.  A shard runs as a
  * pipeline of chunks: a short first chunk (half a regular one) so the kernels
- * start early, then about `chunks` equal chunks of >= 65536 signatures.
+ * start early, then about `chunks` equal chunks of >= 32768 signatures.
  *   PV_STAGING_PINNED   ("pinned", default) each chunk is gathered by up to
  *                       copy_threads host threads into one of two page-locked
  *                       slots per device and DMA'd from there; verdicts come
@@ -263,7 +266,10 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
  *                       hipMemcpyAsync (the runtime stages them).
  * Verdicts are identical either way.  pv_set_host_staging switches every
  * initialised device (A/B timing, tests); copy_threads / chunks 0 keep the
- * current value, otherwise 1..64 / 1..256. */
+ * current value, otherwise 1..64 / 1..256.  Switching to pageable releases the
+ * page-locked slots; with pinned staging each device holds at most two slots of
+ * PV_HOST_PIN_MAX_MB (env, default 512) plus one byte per signature of its
+ * largest shard. */
 #define PV_STAGING_PINNED 0u
 #define PV_STAGING_PAGEABLE 1u
 int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks);

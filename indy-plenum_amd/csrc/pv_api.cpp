@@ -8,10 +8,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -39,14 +43,17 @@ int fail(int code, const char* fmt, ...) {
 
 // host-buffer pipeline (pv_verify_batch): a shard runs as at most
 // PV_HOST_CHUNKS chunks of at least PV_HOST_CHUNK_MIN signatures
-#define PV_HOST_CHUNKS 4
-#define PV_HOST_CHUNK_MIN 65536
+#define PV_HOST_CHUNKS 8
+#define PV_HOST_CHUNK_MIN 32768
+// shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
+#define PV_DEDUP_SAMPLE_MIN 262144
 // chunk gathers into the pinned staging ring use up to this many host threads
 // (PV_HOST_COPY_THREADS overrides); gathers under PV_HOST_PAR_MIN bytes stay on
 // the calling thread
 #define PV_HOST_COPY_THREADS 8
 #define PV_HOST_PAR_MIN (4u << 20)
-// largest page-locked staging slot (two per device)
+// largest page-locked staging slot (two per device, plus the shard's verdicts):
+// at most ~1 GiB of locked host memory per device while pinned staging is on
 #define PV_HOST_PIN_MAX (size_t(512) << 20)
 
 #define HIP_OK(expr)                                                                          \
@@ -99,51 +106,128 @@ struct PinBuf {
 };
 
 // host -> host copies of one chunk's inputs, split over `threads` threads by
-// byte range of the concatenated jobs
+// byte range of the concatenated jobs.  A job with `rebase` set copies u64
+// values minus `rebase` (the chunk's message offsets made shard-relative while
+// they are gathered: no separate pass over all offsets before the first DMA);
+// it must be the FIRST job, so that the 8-byte-multiple piece boundaries never
+// split one of its values between two threads.
 struct CopyJob {
   uint8_t* dst;
   const uint8_t* src;
-  size_t n;
+  size_t n;            // bytes (a multiple of 8 for rebased jobs)
+  uint64_t rebase = 0;
+  bool u64 = false;
 };
 
-void gather(const CopyJob* jobs, int nj, int threads) {
-  size_t total = 0;
-  for (int j = 0; j < nj; ++j) total += jobs[j].n;
-  auto run = [&](size_t a, size_t b) {
-    size_t base = 0;
-    for (int j = 0; j < nj && base < b; base += jobs[j].n, ++j) {
-      const size_t lo = std::max(a, base), hi = std::min(b, base + jobs[j].n);
-      if (lo < hi) memcpy(jobs[j].dst + (lo - base), jobs[j].src + (lo - base), hi - lo);
-    }
-  };
-  if (threads <= 1 || total < PV_HOST_PAR_MIN) {
-    run(0, total);
+// rebased u64 jobs also check that the values never decrease (message
+// offsets): *bad is set, the caller refuses the chunk before any kernel reads it
+void copy_part(const CopyJob& j, size_t lo, size_t hi, std::atomic<bool>* bad) {
+  if (!j.u64) {
+    memcpy(j.dst + lo, j.src + lo, hi - lo);
     return;
   }
-  // no exception crosses the ABI: a thread that cannot be started leaves its
-  // range to the calling thread
-  std::vector<std::thread> ts;
-  std::vector<std::pair<size_t, size_t>> left;
-  const size_t piece = (total + threads - 1) / threads;
-  try {
-    ts.reserve(threads - 1);
-    left.reserve(threads);
-  } catch (...) {
-    run(0, total);
-    return;
+  const uint64_t* a = reinterpret_cast<const uint64_t*>(j.src + lo);
+  uint64_t* b = reinterpret_cast<uint64_t*>(j.dst + lo);
+  uint64_t prev = lo ? a[-1] : a[0];
+  bool dec = false;
+  for (size_t k = 0; k < (hi - lo) / 8; ++k) {
+    dec |= a[k] < prev;
+    prev = a[k];
+    b[k] = a[k] - j.rebase;
   }
-  for (int t = 1; t < threads; ++t) {
-    const size_t a = std::min(total, piece * t), b = std::min(total, piece * (t + 1));
-    try {
-      ts.emplace_back(run, a, b);
-    } catch (...) {
-      left.emplace_back(a, b);
-    }
-  }
-  run(0, std::min(total, piece));
-  for (auto& r : left) run(r.first, r.second);
-  for (auto& t : ts) t.join();
+  if (dec && bad) bad->store(true, std::memory_order_relaxed);
 }
+
+void gather_range(const CopyJob* jobs, int nj, size_t a, size_t b, std::atomic<bool>* bad) {
+  size_t base = 0;
+  for (int j = 0; j < nj && base < b; base += jobs[j].n, ++j) {
+    const size_t lo = std::max(a, base) - base, hi = std::min(b, base + jobs[j].n) - base;
+    if (lo < hi) copy_part(jobs[j], lo, hi, bad);
+  }
+}
+
+// Persistent gather threads of one device (the host pipeline gathers every
+// chunk: starting threads per chunk cost ~20 us each).  run() splits the
+// concatenated jobs into `threads` pieces of 8-byte multiples; piece 0 runs on
+// the caller.  Threads are started lazily; one that cannot be started leaves
+// its pieces to the caller (no exception crosses the ABI).  Used by one
+// thread at a time (a device's shard worker).
+struct GatherPool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, cv_done;
+  const CopyJob* jobs = nullptr;
+  int nj = 0, pieces = 0;
+  size_t total = 0, piece = 0;
+  std::atomic<bool>* bad = nullptr;
+  uint64_t gen = 0;
+  int pending = 0;
+  bool stop = false;
+
+  void worker(int t) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || gen != seen; });
+      if (stop) return;
+      seen = gen;
+      const bool mine = t < pieces;
+      const size_t a = std::min(total, piece * t), b = std::min(total, piece * (t + 1));
+      const CopyJob* J = jobs;
+      const int n = nj;
+      std::atomic<bool>* flag = bad;
+      lk.unlock();
+      if (mine) gather_range(J, n, a, b, flag);
+      lk.lock();
+      if (--pending == 0) cv_done.notify_one();
+    }
+  }
+
+  void run(const CopyJob* js, int n, int threads, std::atomic<bool>* flag) {
+    size_t tot = 0;
+    for (int j = 0; j < n; ++j) tot += js[j].n;
+    if (threads <= 1 || tot < PV_HOST_PAR_MIN) {
+      gather_range(js, n, 0, tot, flag);
+      return;
+    }
+    while ((int)th.size() < threads - 1) {
+      try {
+        th.emplace_back(&GatherPool::worker, this, (int)th.size() + 1);
+      } catch (...) {
+        break;
+      }
+    }
+    const int p = (int)th.size() + 1;
+    const size_t pc = ((tot + p - 1) / p + 7) & ~size_t(7);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      jobs = js;
+      nj = n;
+      total = tot;
+      piece = pc;
+      pieces = p;
+      bad = flag;
+      pending = (int)th.size();
+      ++gen;
+    }
+    cv.notify_all();
+    gather_range(js, n, 0, std::min(tot, pc), flag);
+    std::unique_lock<std::mutex> lk(mu);
+    cv_done.wait(lk, [&] { return pending == 0; });
+  }
+
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+    th.clear();
+    stop = false;
+  }
+  ~GatherPool() { shutdown(); }  // idle threads never outlive the pool (process exit included)
+};
 
 // Distinct 32-byte keys of a host batch (PV_FLAG_DEDUP_KEYS): open addressing
 // with linear probing over 32-bit slots (0 = empty, else 1 + distinct index),
@@ -187,6 +271,28 @@ struct KeyIndex {
 // sharing one inversion).  Verdicts are identical in every mode.
 enum class CurveMode { Half, Full, Grouped };
 
+// Verify workspaces and the compute stream they are used on.  Device-pointer
+// calls use ws[0] (stream = the device stream or the caller's); the host-buffer
+// pipeline alternates chunks over ws[0] and ws[1] on two compute streams, so
+// the kernels of chunk c + 1 fill the tail of chunk c's persistent grid
+// instead of waiting for it (the scratch of concurrently running curve grids
+// must not alias: one per workspace).
+struct Workspace {
+  hipStream_t stream = nullptr;
+  DevBuf<uint32_t> scratch;            // per-lane A / -R tables for the persistent curve grid
+  DevBuf<uint32_t> h;                  // SHA-512 digest, 16 words per signature
+  DevBuf<unsigned long long> counter;  // hash-kernel work queue
+  DevBuf<uint8_t> pre;
+  DevBuf<uint64_t> bitmap;
+  DevBuf<uint32_t> hrec, dlist;        // lattice records, deferred indices (half-size path)
+  DevBuf<unsigned long long> qc;       // [0] deferred count, [1] curve task queue
+  bool half_ran = false;               // qc[0] holds the last generic batch's deferred count
+  void release() {
+    scratch.release(); h.release(); counter.release(); pre.release(); bitmap.release();
+    hrec.release(); dlist.release(); qc.release();
+  }
+};
+
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
@@ -198,21 +304,24 @@ struct Device {
   bool pinned = true;
   int copy_threads = PV_HOST_COPY_THREADS;
   int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
+  size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
   PinBuf pin[2];
+  std::shared_ptr<GatherPool> pool = std::make_shared<GatherPool>();  // host gather threads
   PinBuf vout;  // page-locked verdicts of the shard (D2H target; copied to the caller after the drain)
   hipEvent_t staged[2] = {nullptr, nullptr};  // slot i's H2D has finished
+  hipEvent_t keys_ready = nullptr;            // prepared-key table built (host pipeline, ws[0] -> ws[1])
   int cu_count = 0;
   int curve_blocks = 0;
   int hash_blocks = 0;
   DevBuf<uint32_t> btab;
   DevBuf<uint32_t> bw;        // radix-2^16 base-point chunk tables (half-size path, keyed comb)
-  DevBuf<uint32_t> scratch;   // per-lane A tables for the persistent curve grid
-  DevBuf<uint32_t> h;         // SHA-512 digest, 16 words per signature
-  DevBuf<unsigned long long> counter;  // hash-kernel work queue
-  DevBuf<uint8_t> pre;
+  Workspace ws[2];
+  int last_ws = 0;            // workspace of the last generic verify (pv_curve_stats)
+  size_t scratch_words = 0;   // per-workspace curve scratch
+  DevBuf<unsigned long long> counter;  // SHA-256 work queue
   // staging for host-memory calls
   DevBuf<uint8_t> pk, sig, blob, verdict, tamper;
-  DevBuf<uint64_t> off, bitmap, batch_off;
+  DevBuf<uint64_t> off, batch_off;
   DevBuf<uint32_t> sender, votes;
   DevBuf<uint32_t> tflag, tbits;  // tally: out-of-range sender flag; staged voter bitmaps
   DevBuf<uint8_t> reached;
@@ -222,12 +331,8 @@ struct Device {
   DevBuf<uint32_t> mk0, mk1;    // Merkle level ping-pong / leaf digests
   int sha256_blocks = 0;
   int curve_blocks_keyed = 0;
-  // generic (unkeyed) batches: half-size scalar path (k_lattice + k_curve_half)
-  DevBuf<uint32_t> hrec, dlist;        // lattice records, deferred indices
-  DevBuf<unsigned long long> qc;       // [0] deferred count, [1] curve task queue
   int curve_half_blocks = 0;
   CurveMode mode = CurveMode::Half;
-  bool half_ran = false;               // qc[0] holds the last generic batch's deferred count
   // pv_kernel_timing: HIP-event times of every verify launch while enabled
   bool live_timing = false;
   float live_hash = 0, live_curve = 0;
@@ -256,9 +361,12 @@ Device* find_dev(int id) {
 int init_device(Device& d) {
   HIP_OK(hipSetDevice(d.id));
   HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  d.ws[0].stream = d.stream;
+  HIP_OK(hipStreamCreateWithFlags(&d.ws[1].stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
   HIP_OK(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
   for (auto& e : d.staged) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&d.keys_ready, hipEventDisableTiming));
   if (const char* m = getenv("PV_HOST_STAGING")) {
     if (!strcmp(m, "pageable")) d.pinned = false;
     else if (strcmp(m, "pinned") != 0) return fail(PV_EINVAL, "PV_HOST_STAGING must be pinned or pageable (got %s)", m);
@@ -266,6 +374,11 @@ int init_device(Device& d) {
   if (const char* t = getenv("PV_HOST_CHUNKS")) {
     d.host_chunks = atoi(t);
     if (d.host_chunks < 1 || d.host_chunks > 256) return fail(PV_EINVAL, "PV_HOST_CHUNKS must be in 1..256 (got %s)", t);
+  }
+  if (const char* t = getenv("PV_HOST_PIN_MAX_MB")) {
+    const long mb = atol(t);
+    if (mb < 16 || mb > 4096) return fail(PV_EINVAL, "PV_HOST_PIN_MAX_MB must be in 16..4096 (got %s)", t);
+    d.pin_max = size_t(mb) << 20;
   }
   if (const char* t = getenv("PV_HOST_COPY_THREADS")) {
     d.copy_threads = atoi(t);
@@ -293,9 +406,10 @@ int init_device(Device& d) {
   d.curve_half_blocks = d.cu_count * halfper;
   {
     const size_t a = (size_t)d.curve_blocks * pv::ATAB_WORDS, b = (size_t)d.curve_half_blocks * pv::HALF_SCRATCH_WORDS;
-    HIP_OK(d.scratch.ensure((a > b ? a : b) * pv::CURVE_BLOCK));
+    d.scratch_words = (a > b ? a : b) * pv::CURVE_BLOCK;
+    HIP_OK(d.ws[0].scratch.ensure(d.scratch_words));
   }
-  HIP_OK(d.qc.ensure(2));
+  HIP_OK(d.ws[0].qc.ensure(2));
   if (const char* m = getenv("PV_CURVE_MODE")) {
     if (!strcmp(m, "full")) d.mode = CurveMode::Full;
     else if (!strcmp(m, "grouped")) d.mode = CurveMode::Grouped;
@@ -314,6 +428,7 @@ int init_device(Device& d) {
   if (hper < 1) hper = 1;
   d.hash_blocks = d.cu_count * hper;
   HIP_OK(d.counter.ensure(1));
+  HIP_OK(d.ws[0].counter.ensure(1));
   for (auto& e : d.ev) HIP_OK(hipEventCreate(&e));
   HIP_OK(hipStreamSynchronize(d.stream));
   return PV_OK;
@@ -323,12 +438,15 @@ void release_device(Device& d) {
   if (d.id < 0) return;
   (void)hipSetDevice(d.id);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
-  d.btab.release(); d.bw.release(); d.scratch.release(); d.h.release(); d.pre.release(); d.counter.release();
+  if (d.ws[1].stream) (void)hipStreamSynchronize(d.ws[1].stream);
+  d.btab.release(); d.bw.release(); d.counter.release();
+  for (auto& w : d.ws) w.release();
+  if (d.ws[1].stream) (void)hipStreamDestroy(d.ws[1].stream);
+  d.ws[1].stream = d.ws[0].stream = nullptr;
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
-  d.off.release(); d.bitmap.release(); d.batch_off.release();
+  d.off.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release(); d.tflag.release(); d.tbits.release();
   d.ktab.release(); d.kidx.release(); d.kscr.release(); d.mk0.release(); d.mk1.release();
-  d.hrec.release(); d.dlist.release(); d.qc.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   if (d.copied) (void)hipEventDestroy(d.copied);
@@ -336,19 +454,22 @@ void release_device(Device& d) {
   if (d.copy) (void)hipStreamSynchronize(d.copy), (void)hipStreamDestroy(d.copy);
   for (auto& e : d.staged)
     if (e) (void)hipEventDestroy(e), e = nullptr;
+  if (d.keys_ready) (void)hipEventDestroy(d.keys_ready);
+  d.keys_ready = nullptr;
   d.pin[0].release();
   d.pin[1].release();
   d.vout.release();
+  if (d.pool) d.pool->shutdown();
   d.copy = nullptr;
   if (d.stream) (void)hipStreamDestroy(d.stream);
   d.stream = nullptr;
   d.id = -1;
 }
 
-// enqueue hash + curve for device-resident inputs on stream s
-int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
-                   uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed, float* ms_hash,
-                   float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
+// enqueue hash + curve for device-resident inputs on stream s with workspace w
+int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
+                   const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed,
+                   float* ms_hash, float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
   if (n == 0) return PV_OK;
   const bool live = !timed && d.live_timing;
   if (live) {
@@ -357,33 +478,37 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
     ms_curve = &d.live_curve;
     ++d.live_launches;
   }
-  HIP_OK(d.h.ensure(n * 16));
-  HIP_OK(d.pre.ensure(n));
+  HIP_OK(w.h.ensure(n * 16));
+  HIP_OK(w.pre.ensure(n));
+  HIP_OK(w.counter.ensure(1));
+  HIP_OK(w.qc.ensure(2));
+  HIP_OK(w.scratch.ensure(d.scratch_words));
   uint64_t* bm = bitmap;
   if (!bm) {
-    HIP_OK(d.bitmap.ensure((n + 63) / 64));
-    bm = d.bitmap.p;
+    HIP_OK(w.bitmap.ensure((n + 63) / 64));
+    bm = w.bitmap.p;
   }
   const bool half = !ktab && d.mode != CurveMode::Grouped;
   if (half) {
     if (n > 0xffffffffull) return fail(PV_EINVAL, "at most 2^32-1 signatures per device call");
-    HIP_OK(d.hrec.ensure(n * pv::HSREC_WORDS));
-    HIP_OK(d.dlist.ensure(n));
+    HIP_OK(w.hrec.ensure(n * pv::HSREC_WORDS));
+    HIP_OK(w.dlist.ensure(n));
   }
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
-  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, d.counter.p, d.h.p, d.pre.p, d.hash_blocks, s, kidx));
+  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, w.counter.p, w.h.p, w.pre.p, d.hash_blocks, s, kidx));
   // the "hash" interval also holds the scalar stage of the half-size path
   if (half)
-    HIP_OK(pv::launch_lattice(sig, d.h.p, d.pre.p, n, d.hrec.p, d.dlist.p, d.qc.p, d.qc.p + 1, bm,
+    HIP_OK(pv::launch_lattice(sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
                               d.mode == CurveMode::Full, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (half) {
-    HIP_OK(pv::launch_curve_half(pk, sig, d.h.p, d.hrec.p, d.btab.p, d.bw.p, d.scratch.p,
-                                 d.scratch.cap / pv::HALF_SCRATCH_WORDS, verdict, bm, n, d.dlist.p, d.qc.p, d.qc.p + 1,
+    HIP_OK(pv::launch_curve_half(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
+                                 w.scratch.cap / pv::HALF_SCRATCH_WORDS, verdict, bm, n, w.dlist.p, w.qc.p, w.qc.p + 1,
                                  d.curve_half_blocks, s));
-    d.half_ran = true;
+    w.half_ran = true;
+    d.last_ws = (int)(&w - d.ws);
   } else {
-    HIP_OK(pv::launch_curve(pk, sig, d.h.p, d.pre.p, d.btab.p, d.scratch.p, d.scratch.cap / pv::ATAB_WORDS, verdict,
+    HIP_OK(pv::launch_curve(pk, sig, w.h.p, w.pre.p, d.btab.p, w.scratch.p, w.scratch.cap / pv::ATAB_WORDS, verdict,
                             bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p));
   }
   if (timed) {
@@ -395,6 +520,201 @@ int enqueue_verify(Device& d, const uint8_t* pk, const uint8_t* sig, const uint8
     if (ms_hash) *ms_hash += a;
     if (ms_curve) *ms_curve += b;
   }
+  return PV_OK;
+}
+
+struct HostBatch {
+  const uint8_t* pk;
+  const uint8_t* sig;
+  const uint8_t* blob;
+  const uint64_t* off;
+  uint8_t* verdict;
+  uint32_t flags;
+};
+
+// One device's shard [s, e) of a host-buffer batch (pv_verify_batch), on the
+// calling thread: key dedup and buffers, then a pipeline of chunks.  Chunk c's
+// inputs are gathered by host threads into page-locked slot c & 1 (its
+// offsets rebased to the shard and checked while they are copied), DMA'd on
+// the copy stream, and verified on compute stream c & 1 with workspace c & 1:
+// chunk c + 1's kernels start while chunk c's curve grid drains, so chunked
+// launches pay no tail.  Verdicts come back through a page-locked buffer.
+// Returns after every verdict of the shard is in hb.verdict (or on error,
+// after the device has drained).
+int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
+  const uint64_t m = e - s;
+  if (m == 0) return PV_OK;
+  HIP_OK(hipSetDevice(d.id));
+  // on every exit (errors included) wait for the work that reads host memory
+  struct Drain {
+    Device& d;
+    ~Drain() {
+      (void)hipSetDevice(d.id);
+      (void)hipStreamSynchronize(d.copy);
+      for (auto& w : d.ws) (void)hipStreamSynchronize(w.stream);
+    }
+  } drain{d};
+  const uint8_t* pk = hb.pk;
+  const uint64_t b0 = hb.off[s], bytes = hb.off[e] - b0;
+  // PV_FLAG_DEDUP_KEYS: prepare each distinct key once (cached multiples of
+  // -A) when at least half of the shard's signatures repeat a key
+  std::vector<uint8_t> upk;
+  std::vector<uint32_t> idx;
+  uint64_t nk = m;
+  if (hb.flags & PV_FLAG_DEDUP_KEYS) {
+    // a sample first: s keys (one at a pseudo-random position in each of s
+    // equal strides, so positions never repeat) from a pool of <= m/2
+    // distinct keys in even use repeat ~s^2/m times; a sample with under a
+    // quarter of that means mostly distinct keys, and the full pass is
+    // skipped (the choice only affects speed, never verdicts)
+    KeyIndex ki;
+    bool dedup = true;
+    if (m >= PV_DEDUP_SAMPLE_MIN) {
+      uint64_t smp = 8;
+      while (smp * smp < 64 * m) smp <<= 1;  // s >= 8 sqrt(m): ~64 expected repeats at the threshold
+      const uint64_t stride = m / smp;
+      ki.reset(pk + 32 * s, m);
+      for (uint64_t j = 0; j < smp; ++j) {
+        uint64_t x = (j + 1) * 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        ki.insert(j * stride + (x ^ (x >> 31)) % stride);
+      }
+      dedup = 4 * (smp - ki.first.size()) * m >= smp * smp;
+    }
+    if (dedup) {
+      ki.reset(pk + 32 * s, m);
+      idx.resize(m);
+      for (uint64_t k = 0; k < m && 2 * ki.first.size() <= m; ++k) idx[k] = ki.insert(k);
+      nk = ki.first.size();
+      if (2 * nk > m) {
+        nk = m;
+        idx.clear();
+      } else {
+        upk.resize(nk * 32);
+        for (uint64_t j = 0; j < nk; ++j) memcpy(upk.data() + 32 * j, pk + 32 * (s + ki.first[j]), 32);
+      }
+    }
+  }
+  const bool keyed = !idx.empty();
+  HIP_OK(d.pk.ensure((keyed ? nk : m) * 32));
+  HIP_OK(d.sig.ensure(m * 64));
+  HIP_OK(d.blob.ensure(bytes + 16));
+  HIP_OK(d.off.ensure(m + 1));
+  HIP_OK(d.verdict.ensure(m));
+  // chunk bounds: a short first chunk (half a regular one, >= PV_HOST_CHUNK_MIN)
+  // so the kernels start early, then the rest in equal chunks.  With pinned
+  // staging the chunk count doubles until a chunk's inputs fit one
+  // pin_max slot; a shard whose PV_HOST_CHUNK_MIN-signature chunks still do not
+  // fit (or whose page-locked allocation fails) uses pageable staging.
+  auto chunk_bytes = [&](uint64_t c0, uint64_t c1) -> size_t {
+    return (c1 - c0 + 1) * 8 + (keyed ? 0 : (c1 - c0) * 32) + (c1 - c0) * 64 + (hb.off[s + c1] - hb.off[s + c0]);
+  };
+  std::vector<uint64_t> bounds;
+  size_t cap = 0;
+  for (uint64_t hc = d.host_chunks;; hc *= 2) {
+    const uint64_t reg = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + hc - 1) / hc);
+    const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg / 2));
+    bounds.assign(1, 0);
+    if (hc > 1 && first < m) bounds.push_back(first);
+    const uint64_t rest = m - bounds.back();
+    const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>((rest + reg - 1) / reg, rest / PV_HOST_CHUNK_MIN));
+    const uint64_t c0 = bounds.back();
+    for (uint64_t j = 1; j <= k; ++j) bounds.push_back(c0 + rest * j / k);
+    cap = 0;
+    for (size_t j = 1; j < bounds.size(); ++j) cap = std::max(cap, chunk_bytes(bounds[j - 1], bounds[j]));
+    if (!d.pinned || cap <= d.pin_max || reg == PV_HOST_CHUNK_MIN || hc >= 4096) break;
+  }
+  const size_t nch = bounds.size() - 1;
+  bool pinned = d.pinned && cap <= d.pin_max;
+  if (pinned && (d.pin[0].ensure(cap) != hipSuccess || d.pin[1].ensure(cap) != hipSuccess ||
+                 d.vout.ensure(m) != hipSuccess)) {
+    (void)hipGetLastError();
+    d.pin[0].release();
+    d.pin[1].release();
+    d.vout.release();
+    pinned = false;
+  }
+  std::vector<uint64_t> offs;  // pageable staging: the shard's rebased offsets (read by in-flight copies)
+  if (!pinned) offs.resize(m + 1);
+  HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.copy));
+  if (keyed) {
+    HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
+    HIP_OK(d.kidx.ensure(m));
+    HIP_OK(d.kscr.ensure(nk * pv::KEYTAB_SCRATCH));
+    HIP_OK(hipMemcpyAsync(d.pk.p, upk.data(), nk * 32, hipMemcpyHostToDevice, d.copy));
+    HIP_OK(hipMemcpyAsync(d.kidx.p, idx.data(), m * 4, hipMemcpyHostToDevice, d.copy));
+    HIP_OK(hipEventRecord(d.copied, d.copy));
+    HIP_OK(hipStreamWaitEvent(d.ws[0].stream, d.copied, 0));
+    HIP_OK(pv::launch_keys(d.pk.p, nk, d.ktab.p, d.kscr.p, d.ws[0].stream));
+    HIP_OK(hipEventRecord(d.keys_ready, d.ws[0].stream));
+    HIP_OK(hipStreamWaitEvent(d.ws[1].stream, d.keys_ready, 0));
+  }
+  // PV_HOST_TRACE=1: per-chunk host timings on stderr (pipeline diagnostics)
+  static const bool trace = getenv("PV_HOST_TRACE") && getenv("PV_HOST_TRACE")[0] == '1';
+  const auto tstart = std::chrono::steady_clock::now();
+  auto us = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tstart).count(); };
+  if (trace) fprintf(stderr, "[pv host] dev %d shard %llu sigs: setup %.1f us, %zu chunks, pinned %d\n", d.id,
+                     (unsigned long long)m, us(), nch, (int)pinned);
+  for (size_t c = 0; c < nch; ++c) {
+    const uint64_t c0 = bounds[c], c1 = bounds[c + 1], mc = c1 - c0;
+    Workspace& w = d.ws[c & 1];
+    const double t_begin = trace ? us() : 0;
+    double t_slot = 0, t_gather = 0;
+    const uint64_t cb0 = hb.off[s + c0] - b0, cbytes = hb.off[s + c1] - hb.off[s + c0];
+    const uint8_t* src_pk = pk + 32 * (s + c0);
+    const uint8_t* src_sig = hb.sig + 64 * (s + c0);
+    const uint8_t* src_blob = hb.blob ? hb.blob + b0 + cb0 : nullptr;
+    const uint8_t* src_off;
+    std::atomic<bool> bad{false};
+    if (pinned) {
+      // gather the chunk into slot c & 1 once its previous H2D (chunk c - 2) is done
+      const int slot = (int)(c & 1);
+      if (c >= 2) HIP_OK(hipEventSynchronize(d.staged[slot]));
+      if (trace) t_slot = us();
+      uint8_t* base = d.pin[slot].p;
+      uint8_t *p_off = base, *p_pk = p_off + (mc + 1) * 8, *p_sig = p_pk + (keyed ? 0 : mc * 32),
+              *p_blob = p_sig + mc * 64;
+      const CopyJob jobs[4] = {{p_off, reinterpret_cast<const uint8_t*>(hb.off + s + c0), (mc + 1) * 8, b0, true},
+                               {p_pk, src_pk, keyed ? 0 : mc * 32},
+                               {p_sig, src_sig, mc * 64},
+                               {p_blob, src_blob, cbytes}};
+      d.pool->run(jobs, 4, d.copy_threads, &bad);
+      if (trace) t_gather = us();
+      src_off = p_off;
+      src_pk = p_pk;
+      src_sig = p_sig;
+      src_blob = p_blob;
+    } else {
+      const CopyJob job{reinterpret_cast<uint8_t*>(offs.data() + c0), reinterpret_cast<const uint8_t*>(hb.off + s + c0),
+                        (mc + 1) * 8, b0, true};
+      gather_range(&job, 1, 0, job.n, &bad);
+      src_off = reinterpret_cast<const uint8_t*>(offs.data() + c0);
+    }
+    if (bad.load()) return fail(PV_EINVAL, "msg_off not monotone in [%llu, %llu]", (unsigned long long)(s + c0),
+                                (unsigned long long)(s + c1));
+    if (!keyed) HIP_OK(hipMemcpyAsync(d.pk.p + 32 * c0, src_pk, mc * 32, hipMemcpyHostToDevice, d.copy));
+    HIP_OK(hipMemcpyAsync(d.sig.p + 64 * c0, src_sig, mc * 64, hipMemcpyHostToDevice, d.copy));
+    if (cbytes) HIP_OK(hipMemcpyAsync(d.blob.p + cb0, src_blob, cbytes, hipMemcpyHostToDevice, d.copy));
+    HIP_OK(hipMemcpyAsync(d.off.p + c0, src_off, (mc + 1) * 8, hipMemcpyHostToDevice, d.copy));
+    if (pinned) HIP_OK(hipEventRecord(d.staged[c & 1], d.copy));
+    HIP_OK(hipEventRecord(d.copied, d.copy));
+    HIP_OK(hipStreamWaitEvent(w.stream, d.copied, 0));
+    // blob base + shard-relative offsets: the hash kernel reads blob + off[i]
+    int rc = enqueue_verify(d, w, keyed ? d.pk.p : d.pk.p + 32 * c0, d.sig.p + 64 * c0, d.blob.p, d.off.p + c0, mc,
+                            d.verdict.p + c0, nullptr, w.stream, false, nullptr, nullptr, keyed ? d.ktab.p : nullptr,
+                            keyed ? d.kidx.p + c0 : nullptr);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(pinned ? d.vout.p + c0 : hb.verdict + s + c0, d.verdict.p + c0, mc, hipMemcpyDeviceToHost,
+                          w.stream));
+    if (trace)
+      fprintf(stderr, "[pv host] chunk %zu (%llu sigs): begin %.1f slot-free %.1f gathered %.1f enqueued %.1f us\n", c,
+              (unsigned long long)mc, t_begin, t_slot, t_gather, us());
+  }
+  HIP_OK(hipStreamSynchronize(d.copy));
+  for (auto& w : d.ws) HIP_OK(hipStreamSynchronize(w.stream));
+  if (pinned) memcpy(hb.verdict + s, d.vout.p, m);
+  if (trace) fprintf(stderr, "[pv host] drained %.1f us\n", us());
   return PV_OK;
 }
 
@@ -455,203 +775,39 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
   if (n == 0) return PV_OK;
   if (!pk || !sig || !msg_off || !verdict || (!msg_blob && msg_off[n] != msg_off[0]))
     return fail(PV_EINVAL, "null buffer");
-  for (uint64_t i = 0; i < n; ++i)
-    if (msg_off[i + 1] < msg_off[i]) return fail(PV_EINVAL, "msg_off not monotone at %llu", (unsigned long long)i);
+  if (msg_off[n] < msg_off[0]) return fail(PV_EINVAL, "msg_off not monotone");
   std::vector<Device*> devs = select_devs(device_mask);
   if (devs.empty()) return fail(PV_ENODEV, "device_mask 0x%x selects no initialised device", device_mask);
+  const HostBatch hb{pk, sig, msg_blob, msg_off, verdict, flags};
   const uint64_t G = devs.size();
-  // Per device: one shard [s, e).  Setup (offsets, key dedup, buffers, key
-  // preparation) first; then the shard runs as a pipeline of chunks: chunk c's
-  // inputs go H2D on the copy stream, the compute stream waits for them, runs
-  // hash + curve and copies the chunk's verdicts back.  The pageable H2D of
-  // chunk c + 1 (staged by the runtime on the host thread) then overlaps the
-  // kernels of chunk c.  Chunks index into the shard's buffers (offsets stay
-  // shard-relative), so no device buffer is reused while in flight.  With
-  // pinned staging (default) the H2D is a DMA from a page-locked slot: host
-  // threads gather chunk c + 1 into the other slot while chunk c's DMA and
-  // chunk c - 1's kernels run.
-  struct Shard {
-    uint64_t s = 0, m = 0;
-    std::vector<uint64_t> bounds;  // chunk c = [bounds[c], bounds[c + 1])
-    std::vector<uint64_t> offs;
-    std::vector<uint8_t> upk;
-    std::vector<uint32_t> idx;
-    bool keyed = false;
-    bool pinned = false;  // this shard's chunks go through the pinned staging ring
+  if (G == 1) return run_shard(*devs[0], hb, 0, n);
+  // one worker thread per device: each gathers, stages and launches its own
+  // shard, so no device waits on another's host gathers (errors come back as
+  // codes + messages; no exception crosses the ABI)
+  std::vector<int> rc(G, PV_OK);
+  std::vector<std::string> err(G);
+  std::vector<std::thread> ts;
+  auto work = [&](uint64_t g) {
+    rc[g] = run_shard(*devs[g], hb, n * g / G, n * (g + 1) / G);
+    if (rc[g]) err[g] = g_err;
   };
-  std::vector<Shard> sh(G);
-  // on every exit (errors included) wait for the copies that read `sh` and the caller's buffers
-  struct Drain {
-    std::vector<Device*>& v;
-    ~Drain() {
-      for (Device* d : v) {
-        (void)hipSetDevice(d->id);
-        (void)hipStreamSynchronize(d->copy);
-        (void)hipStreamSynchronize(d->stream);
-      }
-    }
-  } drain{devs};
-  uint64_t max_chunks = 0;
-  for (uint64_t g = 0; g < G; ++g) {
-    Device& d = *devs[g];
-    Shard& z = sh[g];
-    const uint64_t s = n * g / G, e = n * (g + 1) / G, m = e - s;
-    z.s = s;
-    z.m = m;
-    if (m == 0) continue;
-    HIP_OK(hipSetDevice(d.id));
-    const uint64_t b0 = msg_off[s], bytes = msg_off[e] - b0;
-    z.offs.resize(m + 1);
-    for (uint64_t k = 0; k <= m; ++k) z.offs[k] = msg_off[s + k] - b0;
-    // PV_FLAG_DEDUP_KEYS: prepare each distinct key once (cached multiples of
-    // -A) when at least half of the shard's signatures repeat a key
-    uint64_t nk = m;
-    if (flags & PV_FLAG_DEDUP_KEYS) {
-      // a sample first: s keys (one at a pseudo-random position in each of s
-      // equal strides, so positions never repeat) from a pool of <= m/2
-      // distinct keys in even use repeat ~s^2/m times; a sample with under a
-      // quarter of that means mostly distinct keys, and the full pass is
-      // skipped (the choice only affects speed, never verdicts)
-      KeyIndex ki;
-      bool dedup = true;
-      if (m >= 4 * PV_HOST_CHUNK_MIN) {
-        uint64_t smp = 8;
-        while (smp * smp < 64 * m) smp <<= 1;  // s >= 8 sqrt(m): ~64 expected repeats at the threshold
-        const uint64_t stride = m / smp;
-        ki.reset(pk + 32 * s, m);
-        for (uint64_t j = 0; j < smp; ++j) {
-          uint64_t x = (j + 1) * 0x9E3779B97F4A7C15ull;
-          x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-          x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-          ki.insert(j * stride + (x ^ (x >> 31)) % stride);
-        }
-        dedup = 4 * (smp - ki.first.size()) * m >= smp * smp;
-      }
-      if (dedup) {
-        ki.reset(pk + 32 * s, m);
-        z.idx.resize(m);
-        for (uint64_t k = 0; k < m && 2 * ki.first.size() <= m; ++k) z.idx[k] = ki.insert(k);
-        nk = ki.first.size();
-        if (2 * nk > m) {
-          nk = m;
-          z.idx.clear();
-        } else {
-          z.upk.resize(nk * 32);
-          for (uint64_t j = 0; j < nk; ++j) memcpy(z.upk.data() + 32 * j, pk + 32 * (s + ki.first[j]), 32);
-        }
-      }
-    }
-    z.keyed = !z.idx.empty();
-    HIP_OK(d.pk.ensure((z.keyed ? nk : m) * 32));
-    HIP_OK(d.sig.ensure(m * 64));
-    HIP_OK(d.blob.ensure(bytes + 16));
-    HIP_OK(d.off.ensure(m + 1));
-    HIP_OK(d.verdict.ensure(m));
-    // chunk bounds: a short first chunk (half a regular one, >= PV_HOST_CHUNK_MIN)
-    // so the kernels start early, then the rest in equal chunks.  With pinned
-    // staging the chunk count doubles until a chunk's inputs fit one
-    // PV_HOST_PIN_MAX slot; a shard whose 65536-signature chunks still do not
-    // fit (or whose page-locked allocation fails) uses pageable staging.
-    auto chunk_bytes = [&](uint64_t c0, uint64_t c1) -> size_t {
-      return (c1 - c0 + 1) * 8 + (z.keyed ? 0 : (c1 - c0) * 32) + (c1 - c0) * 64 + (z.offs[c1] - z.offs[c0]);
-    };
-    size_t cap = 0;
-    for (uint64_t hc = d.host_chunks;; hc *= 2) {
-      const uint64_t reg = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + hc - 1) / hc);
-      const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg / 2));
-      z.bounds.assign(1, 0);
-      if (hc > 1 && first < m) z.bounds.push_back(first);
-      const uint64_t rest = m - z.bounds.back();
-      const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>((rest + reg - 1) / reg, rest / PV_HOST_CHUNK_MIN));
-      const uint64_t b0 = z.bounds.back();
-      for (uint64_t j = 1; j <= k; ++j) z.bounds.push_back(b0 + rest * j / k);
-      cap = 0;
-      for (size_t j = 1; j < z.bounds.size(); ++j) cap = std::max(cap, chunk_bytes(z.bounds[j - 1], z.bounds[j]));
-      if (!d.pinned || cap <= PV_HOST_PIN_MAX || reg == PV_HOST_CHUNK_MIN || hc >= 4096) break;
-    }
-    z.pinned = d.pinned && cap <= PV_HOST_PIN_MAX;
-    if (z.pinned && (d.pin[0].ensure(cap) != hipSuccess || d.pin[1].ensure(cap) != hipSuccess ||
-                     d.vout.ensure(m) != hipSuccess)) {
-      (void)hipGetLastError();
-      d.pin[0].release();
-      d.pin[1].release();
-      z.pinned = false;
-    }
-    // workspaces sized for the largest chunk before anything is in flight
-    uint64_t cm = 0;
-    for (size_t j = 1; j < z.bounds.size(); ++j) cm = std::max(cm, z.bounds[j] - z.bounds[j - 1]);
-    HIP_OK(d.h.ensure(cm * 16));
-    HIP_OK(d.pre.ensure(cm));
-    HIP_OK(d.bitmap.ensure((cm + 63) / 64));
-    HIP_OK(d.hrec.ensure(cm * pv::HSREC_WORDS));
-    HIP_OK(d.dlist.ensure(cm));
-    max_chunks = std::max<uint64_t>(max_chunks, z.bounds.size() - 1);
-    HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.copy));
-    if (z.keyed) {
-      HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
-      HIP_OK(d.kidx.ensure(m));
-      HIP_OK(d.kscr.ensure(nk * pv::KEYTAB_SCRATCH));
-      HIP_OK(hipMemcpyAsync(d.pk.p, z.upk.data(), nk * 32, hipMemcpyHostToDevice, d.copy));
-      HIP_OK(hipMemcpyAsync(d.kidx.p, z.idx.data(), m * 4, hipMemcpyHostToDevice, d.copy));
-      HIP_OK(hipEventRecord(d.copied, d.copy));
-      HIP_OK(hipStreamWaitEvent(d.stream, d.copied, 0));
-      HIP_OK(pv::launch_keys(d.pk.p, nk, d.ktab.p, d.kscr.p, d.stream));
+  std::vector<uint64_t> inline_g;
+  try {
+    ts.reserve(G);
+  } catch (...) {
+  }
+  for (uint64_t g = 1; g < G; ++g) {
+    try {
+      ts.emplace_back(work, g);
+    } catch (...) {
+      inline_g.push_back(g);
     }
   }
-  // chunk-major over devices, so every device's pipeline starts early
-  for (uint64_t c = 0; c < max_chunks; ++c) {
-    for (uint64_t g = 0; g < G; ++g) {
-      Device& d = *devs[g];
-      Shard& z = sh[g];
-      if (c + 1 >= z.bounds.size()) continue;
-      const uint64_t c0 = z.bounds[c];
-      const uint64_t c1 = z.bounds[c + 1], mc = c1 - c0;
-      HIP_OK(hipSetDevice(d.id));
-      const uint64_t b0 = msg_off[z.s], cb0 = z.offs[c0], cbytes = z.offs[c1] - cb0;
-      const uint8_t* src_off = reinterpret_cast<const uint8_t*>(z.offs.data() + c0);
-      const uint8_t* src_pk = pk + 32 * (z.s + c0);
-      const uint8_t* src_sig = sig + 64 * (z.s + c0);
-      const uint8_t* src_blob = msg_blob ? msg_blob + b0 + cb0 : nullptr;
-      if (z.pinned) {
-        // gather the chunk into slot c & 1 once its previous H2D (chunk c - 2) is done
-        const int slot = (int)(c & 1);
-        if (c >= 2) HIP_OK(hipEventSynchronize(d.staged[slot]));
-        uint8_t* base = d.pin[slot].p;
-        uint8_t *p_off = base, *p_pk = p_off + (mc + 1) * 8, *p_sig = p_pk + (z.keyed ? 0 : mc * 32),
-                *p_blob = p_sig + mc * 64;
-        const CopyJob jobs[4] = {{p_off, src_off, (mc + 1) * 8},
-                                 {p_pk, src_pk, z.keyed ? 0 : mc * 32},
-                                 {p_sig, src_sig, mc * 64},
-                                 {p_blob, src_blob, cbytes}};
-        gather(jobs, 4, d.copy_threads);
-        src_off = p_off;
-        src_pk = p_pk;
-        src_sig = p_sig;
-        src_blob = p_blob;
-      }
-      if (!z.keyed) HIP_OK(hipMemcpyAsync(d.pk.p + 32 * c0, src_pk, mc * 32, hipMemcpyHostToDevice, d.copy));
-      HIP_OK(hipMemcpyAsync(d.sig.p + 64 * c0, src_sig, mc * 64, hipMemcpyHostToDevice, d.copy));
-      if (cbytes) HIP_OK(hipMemcpyAsync(d.blob.p + cb0, src_blob, cbytes, hipMemcpyHostToDevice, d.copy));
-      HIP_OK(hipMemcpyAsync(d.off.p + c0, src_off, (mc + 1) * 8, hipMemcpyHostToDevice, d.copy));
-      if (z.pinned) HIP_OK(hipEventRecord(d.staged[c & 1], d.copy));
-      HIP_OK(hipEventRecord(d.copied, d.copy));
-      HIP_OK(hipStreamWaitEvent(d.stream, d.copied, 0));
-      // blob base + shard-relative offsets: the hash kernel reads blob + off[i]
-      int rc = enqueue_verify(d, z.keyed ? d.pk.p : d.pk.p + 32 * c0, d.sig.p + 64 * c0, d.blob.p, d.off.p + c0, mc,
-                              d.verdict.p + c0, nullptr, d.stream, false, nullptr, nullptr,
-                              z.keyed ? d.ktab.p : nullptr, z.keyed ? d.kidx.p + c0 : nullptr);
-      if (rc) return rc;
-      HIP_OK(hipMemcpyAsync(z.pinned ? d.vout.p + c0 : verdict + z.s + c0, d.verdict.p + c0, mc,
-                            hipMemcpyDeviceToHost, d.stream));
-    }
-  }
-  // drain (the staging vectors in `sh` outlive every copy that reads them)
-  for (uint64_t g = 0; g < G; ++g) {
-    HIP_OK(hipSetDevice(devs[g]->id));
-    HIP_OK(hipStreamSynchronize(devs[g]->copy));
-    HIP_OK(hipStreamSynchronize(devs[g]->stream));
-    if (sh[g].pinned && sh[g].m) memcpy(verdict + sh[g].s, devs[g]->vout.p, sh[g].m);
-  }
+  work(0);
+  for (uint64_t g : inline_g) work(g);
+  for (auto& t : ts) t.join();
+  for (uint64_t g = 0; g < G; ++g)
+    if (rc[g]) return fail(rc[g], "device %d: %s", devs[g]->id, err[g].c_str());
   return PV_OK;
 }
 
@@ -665,7 +821,7 @@ int pv_verify_batch_device(const uint8_t* pk, const uint8_t* sig, const uint8_t*
   if (!pk || !sig || !msg_blob || !msg_off || !verdict) return fail(PV_EINVAL, "null device buffer");
   HIP_OK(hipSetDevice(device));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
-  int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr);
+  int rc = enqueue_verify(*d, d->ws[0], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr);
   if (rc) return rc;
   HIP_OK(hipStreamSynchronize(s));
   return PV_OK;
@@ -697,7 +853,8 @@ int pv_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const 
   if (!ktab || !key_idx || !pk || !sig || !msg_blob || !msg_off || !verdict) return fail(PV_EINVAL, "null device buffer");
   HIP_OK(hipSetDevice(device));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
-  int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr, ktab, key_idx);
+  int rc = enqueue_verify(*d, d->ws[0], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr, ktab,
+                          key_idx);
   if (rc) return rc;
   HIP_OK(hipStreamSynchronize(s));
   return PV_OK;
@@ -716,7 +873,7 @@ int pv_time_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, c
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   float a = 0, b = 0;
   for (int it = 0; it < iters; ++it) {
-    int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, true, &a, &b, ktab, key_idx);
+    int rc = enqueue_verify(*d, d->ws[0], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, true, &a, &b, ktab, key_idx);
     if (rc) return rc;
   }
   if (ms_hash) *ms_hash = a / iters;
@@ -736,7 +893,7 @@ int pv_time_verify_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   float a = 0, b = 0;
   for (int it = 0; it < iters; ++it) {
-    int rc = enqueue_verify(*d, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, true, &a, &b);
+    int rc = enqueue_verify(*d, d->ws[0], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, true, &a, &b);
     if (rc) return rc;
   }
   if (ms_hash) *ms_hash = a / iters;
@@ -765,7 +922,7 @@ int pv_set_curve_mode(uint32_t mode) {
   if (mode > PV_CURVE_GROUPED) return fail(PV_EINVAL, "unknown curve mode %u", mode);
   for (auto& d : g_devs) {
     d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
-    d.half_ran = false;
+    d.ws[0].half_ran = d.ws[1].half_ran = false;
   }
   return PV_OK;
 }
@@ -776,10 +933,18 @@ int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks) {
   if (mode > PV_STAGING_PAGEABLE) return fail(PV_EINVAL, "unknown staging mode %u", mode);
   if (copy_threads < 0 || copy_threads > 64) return fail(PV_EINVAL, "copy_threads must be in 0..64 (got %d)", copy_threads);
   if (chunks < 0 || chunks > 256) return fail(PV_EINVAL, "chunks must be in 0..256 (got %d)", chunks);
+  DeviceGuard dg;
   for (auto& d : g_devs) {
     d.pinned = mode == PV_STAGING_PINNED;
     if (copy_threads) d.copy_threads = copy_threads;
     if (chunks) d.host_chunks = chunks;
+    if (!d.pinned) {  // pageable staging holds no page-locked memory
+      (void)hipSetDevice(d.id);
+      (void)hipStreamSynchronize(d.copy);
+      d.pin[0].release();
+      d.pin[1].release();
+      d.vout.release();
+    }
   }
   return PV_OK;
 }
@@ -793,10 +958,11 @@ int pv_curve_stats(int device, uint32_t* mode, uint64_t* deferred) {
                                                                                              : PV_CURVE_GROUPED;
   if (deferred) {
     *deferred = 0;
-    if (d->half_ran) {
+    Workspace& w = d->ws[d->last_ws];
+    if (w.half_ran) {
       HIP_OK(hipSetDevice(device));
-      HIP_OK(hipStreamSynchronize(d->stream));
-      HIP_OK(hipMemcpy(deferred, d->qc.p, sizeof(uint64_t), hipMemcpyDeviceToHost));
+      HIP_OK(hipStreamSynchronize(w.stream));
+      HIP_OK(hipMemcpy(deferred, w.qc.p, sizeof(uint64_t), hipMemcpyDeviceToHost));
     }
   }
   return PV_OK;

@@ -165,10 +165,12 @@ def test_keyed_device_path_c3_and_c4(nat):
 @pytest.mark.parametrize('shape', ['c2', 'c4_keyed'])
 def test_host_pipeline_multi_chunk(nat, shape):
     """pv_verify_batch runs a shard as a pipeline of chunks (H2D of chunk c+1 on
-    the copy stream overlaps the kernels of chunk c; >= 65536 signatures per
-    chunk): a 200k batch spans 2-3 chunks.  Verdicts == not tampered; the keyed
-    case (4096-key pool, ragged 128 B - 4 KB payloads) indexes the chunk's
-    key indices and shard-relative message offsets."""
+    the copy stream overlaps the kernels of chunk c, chunks alternate over two
+    compute streams and workspaces; >= 32768 signatures per chunk): a 200k
+    batch spans 1-6 chunks.  Verdicts == not tampered; the keyed case
+    (4096-key pool, ragged 128 B - 4 KB payloads) indexes the chunk's key
+    indices and shard-relative message offsets, with the key table built on
+    stream 0 and consumed on both."""
     from plenum_gpu import synth
     from plenum_gpu.device import SyntheticBatch
     if shape == 'c2':
@@ -180,9 +182,10 @@ def test_host_pipeline_multi_chunk(nat, shape):
     blob = b.blob.cpu().numpy()[:int(off[-1])]
     want = ~b.tamper.cpu().numpy().astype(bool)
     # pinned staging ring with threaded and single-thread gathers (4 chunks:
-    # 65536 + 134464 signatures; 16 chunks: 65536 + 2 x 67232, so chunk 2
-    # waits for slot 0's DMA; the tail case below: 65536 + 65539), one chunk,
-    # and the runtime's pageable staging
+    # 32768 + 2 x 83616 signatures; 16 chunks: 32768 + 5 x ~33446, so chunks
+    # 2.. wait for their slot's previous DMA and reuse a workspace; the tail
+    # case below: 32768 + 3 x ~32769), one chunk, and the runtime's pageable
+    # staging
     try:
         for staging, threads, chunks in (('pinned', 8, 4), ('pinned', 1, 1), ('pageable', 0, 4), ('pinned', 8, 16)):
             nat.set_host_staging(staging, threads, chunks)
@@ -193,7 +196,27 @@ def test_host_pipeline_multi_chunk(nat, shape):
             got = nat.verify_batch_arrays(pk[:131075], sig[:131075], blob[:int(off[131075])], off[:131076])
             assert (got == want[:131075]).all(), (shape, staging, threads)
     finally:
-        nat.set_host_staging('pinned', 8, 4)
+        nat.set_host_staging('pinned', 8, 8)
+
+
+def test_host_offsets_checked_before_launch(nat):
+    """msg_off is validated chunk by chunk while it is gathered: a decreasing
+    offset in the middle of a multi-chunk shard is PV_EINVAL (no kernel reads
+    it), and the next call on the same device is unaffected."""
+    from plenum_gpu.device import SyntheticBatch
+    b = SyntheticBatch(0, 100000, 64, cfg=2, first=777)
+    pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()
+    off = b.off.cpu().numpy().astype(np.uint64)
+    blob = b.blob.cpu().numpy()[:int(off[-1])]
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    bad = off.copy()
+    bad[70001] = bad[70000] - 1
+    for staging in ('pinned', 'pageable'):
+        nat.set_host_staging(staging, 8, 8)
+        with pytest.raises(nat.PlenumGpuError, match='monotone'):
+            nat.verify_batch_arrays(pk, sig, blob, bad, dedup_keys=False)
+        assert (nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=False) == want).all()
+    nat.set_host_staging('pinned', 8, 8)
 
 
 def test_host_staging_slot_cap(nat):
