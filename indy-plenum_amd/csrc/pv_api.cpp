@@ -495,10 +495,12 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     HIP_OK(w.dlist.ensure(n));
   }
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
-  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, w.counter.p, w.h.p, w.pre.p, d.hash_blocks, s, kidx));
+  // the half-size path runs the pre-checks in k_lattice (k_hash hashes every
+  // signature); keyed and grouped batches in k_precheck before the hash
+  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, w.counter.p, w.h.p, half ? nullptr : w.pre.p, d.hash_blocks, s, kidx));
   // the "hash" interval also holds the scalar stage of the half-size path
   if (half)
-    HIP_OK(pv::launch_lattice(sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
+    HIP_OK(pv::launch_lattice(pk, sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
                               d.mode == CurveMode::Full, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (half) {

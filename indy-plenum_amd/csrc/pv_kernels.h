@@ -33,6 +33,9 @@ hipError_t curve_occupancy(int* blocks_per_cu, bool keyed = false);
 // word the launch resets (work queue).
 hipError_t hash_occupancy(int* blocks_per_cu);
 // kidx (may be NULL): signature i's key is pk[kidx[i]] (keyed batches)
+// pre != null: k_precheck writes the pre-check verdicts first and k_hash skips
+// the rejected signatures; pre == null: every signature is hashed (the
+// half-size path checks in launch_lattice)
 hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
                        unsigned long long* counter, uint32_t* dig, uint8_t* pre, int blocks, hipStream_t s,
                        const uint32_t* kidx = nullptr);
@@ -46,8 +49,9 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
                         const uint32_t* kidx = nullptr, const uint32_t* bw = nullptr);
 
 // Half-size scalar path (generic batches, pv_lattice.h):
-//   launch_lattice   h mod L -> (c, d, s') records (HSREC_WORDS words per
-//                    signature), deferred indices -> dlist / *dcount; also
+//   launch_lattice   pre-checks (-> pre) and h mod L -> (c, d, s') records
+//                    (HSREC_WORDS words per signature), deferred indices ->
+//                    dlist / *dcount; also
 //                    zeroes *tasks and the bitmap (ceil(n/64) words) the curve
 //                    kernel ORs into.  n < 2^32.
 //   launch_curve_half  verdicts + bitmap; per-lane scratch HALF_SCRATCH_WORDS
@@ -55,9 +59,9 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
 constexpr int HSREC_WORDS = 20;
 constexpr int HALF_SCRATCH_WORDS = 2 * 9 * 40;
 hipError_t curve_half_occupancy(int* blocks_per_cu);
-hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t* pre, uint64_t n, uint32_t* rec,
-                          uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks, uint64_t* bitmap,
-                          bool force_full, hipStream_t s);
+hipError_t launch_lattice(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, uint8_t* pre, uint64_t n,
+                          uint32_t* rec, uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks,
+                          uint64_t* bitmap, bool force_full, hipStream_t s);
 // btab: the radix-256 base-point tables (deferred full-length tasks); bw:
 // BWTAB_WORDS words, the radix-2^16 chunk tables k * 2^(32 q) * B, q = 0..7
 // (launch_bw_init; chunks 0 and 4 serve the half-size path, all eight the

@@ -59,37 +59,69 @@ __device__ __forceinline__ uint64_t take_index(unsigned long long* counter) {
 #ifndef PV_HASH_WAVES
 #define PV_HASH_WAVES 2
 #endif
+// libsodium's pre-checks on (R, S, A), one
+// lane per signature, ahead of the hash: keeps the branchy, load-dependent
+// check out of k_hash's refill path (which every ragged C4 iteration hit).
+__global__ __launch_bounds__(256) void k_precheck(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                                   uint64_t n, uint8_t* __restrict__ pre,
+                                                   const uint32_t* __restrict__ kidx) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  pre[i] = precheck(pk + 32 * (kidx ? (uint64_t)kidx[i] : i), sig + 64 * i) ? 1 : 0;
+}
+
+// SHA-512(R || A || M) for the signatures that passed the pre-checks (pre =
+// null: every signature; the half-size path runs the pre-checks in k_lattice
+// instead and never reads the digests of rejected ones).  The next message of
+// a lane is taken from the queue one message ahead: its offsets, pre-check
+// verdict and key index are loaded while the current message is hashed, so a
+// refill finds them in registers.
 __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
                                                      const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ off, uint64_t n,
                                                      unsigned long long* __restrict__ counter,
-                                                     uint32_t* __restrict__ dig, uint8_t* __restrict__ pre,
+                                                     uint32_t* __restrict__ dig, const uint8_t* __restrict__ pre,
                                                      const uint32_t* __restrict__ kidx) {
-  uint64_t idx = take_index(counter);
-  uint64_t blk = 0, nblk = 0, mo = 0, ml = 0;
+  uint64_t idx = n, blk = 0, nblk = 0, mo = 0, ml = 0;
   uint64_t hs[8];
-  const uint8_t* A = pk;
+  uint32_t ra[16];   // R || A of the current message (block 0's prefix)
+  // prefetched next message: offsets, pre-check verdict, R || A
+  uint64_t nidx = take_index(counter), nmo = 0, nme = 0;
+  uint32_t nok = 0, nra[16];
+  auto prefetch = [&]() {
+    if (nidx < n) {
+      nmo = off[nidx];
+      nme = off[nidx + 1];
+      nok = pre ? pre[nidx] : 1u;
+      load8(nra, sig + 64 * nidx);
+      load8(nra + 8, pk + 32 * (kidx ? (uint64_t)kidx[nidx] : nidx));
+    }
+  };
+  prefetch();
   while (true) {
-    // refill: skip messages that fail the pre-checks
-    while (blk == nblk && idx < n) {
-      A = pk + 32 * (kidx ? (uint64_t)kidx[idx] : idx);
-      const bool ok = precheck(A, sig + 64 * idx);
-      pre[idx] = ok ? 1 : 0;
+    // refill from the prefetched message, then prefetch the one after it
+    while (blk == nblk && nidx < n) {
+      idx = nidx;
+      const bool ok = nok != 0;
+      mo = nmo;
+      ml = nme - nmo;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ra[j] = nra[j];
+      nidx = take_index(counter);
+      prefetch();
       if (ok) {
-        mo = off[idx];
-        ml = off[idx + 1] - mo;
         nblk = hram_blocks(ml);
         blk = 0;
         sha512_init(hs);
-      } else {
-        idx = take_index(counter);
       }
     }
-    if (idx >= n) break;
-    // (prefetching the next block's words one compression ahead measured no
-    // gain on C4 and a loss on C2: the loads are not what bounds this kernel)
+    if (blk == nblk) break;   // queue drained and no message in progress
     uint64_t w[16];
-    hram_block(w, sig + 64 * idx, A, blob + mo, ml, blk, nblk);
+    {
+      uint32_t y[MSG_Y];
+      msg_fetch(y, blob + mo, ml, hram_q(blk), blk == 0);
+      hram_assemble_ra(w, y, ra, blob + mo, ml, blk, nblk);
+    }
     sha512_compress(hs, w);
     if (++blk == nblk) {
       uint32_t d[16];
@@ -97,7 +129,6 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
       uint32_t* o = dig + 16 * idx;
 #pragma unroll
       for (int k = 0; k < 16; ++k) o[k] = d[k];
-      idx = take_index(counter);
     }
   }
 }
@@ -113,6 +144,11 @@ hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blo
   if (n == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
+  if (pre) {
+    hipLaunchKernelGGL(k_precheck, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, pk, sig, n, pre, kidx);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   const uint64_t need = (n + HASH_BLOCK - 1) / HASH_BLOCK;
   const uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
   hipLaunchKernelGGL(k_hash, dim3((uint32_t)b), dim3(HASH_BLOCK), 0, s, pk, sig, blob, off, n, counter, dig, pre,
@@ -208,13 +244,19 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
 // k_lattice: one lane per signature.  h = digest mod L, Euclid on (8L, h) ->
 // (c, d), s' = d S mod L, written as the record the curve kernel reads;
 // deferred indices (~0.2 %) are appended to `dlist` (wave-aggregated atomic).
-__global__ __launch_bounds__(256) void k_lattice(const uint8_t* __restrict__ sig, const uint32_t* __restrict__ dig,
-                                                  const uint8_t* __restrict__ pre, uint64_t n,
+__global__ __launch_bounds__(256) void k_lattice(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                                  const uint32_t* __restrict__ dig, uint8_t* __restrict__ pre, uint64_t n,
                                                   uint32_t* __restrict__ rec, uint32_t* __restrict__ dlist,
                                                   unsigned long long* __restrict__ dcount, int force_full) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   uint32_t st = HS_NONE;
-  if (i < n) st = lattice_one(rec + HREC_WORDS * i, pre[i] != 0, dig + 16 * i, sig + 64 * i, force_full != 0);
+  if (i < n) {
+    // libsodium's pre-checks (App. C.2 steps 1-3) here, one lane per
+    // signature: k_hash hashed every message of the half-size path
+    const bool ok = precheck(pk + 32 * i, sig + 64 * i);
+    pre[i] = ok ? 1 : 0;
+    st = lattice_one(rec + HREC_WORDS * i, ok, dig + 16 * i, sig + 64 * i, force_full != 0);
+  }
   const bool defer = st == HS_DEFER;
   const uint64_t m = __ballot(defer);
   if (m) {
@@ -283,9 +325,9 @@ hipError_t curve_half_occupancy(int* blocks_per_cu) {
                                                       CURVE_BLOCK, 0);
 }
 
-hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t* pre, uint64_t n, uint32_t* rec,
-                          uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks, uint64_t* bitmap,
-                          bool force_full, hipStream_t s) {
+hipError_t launch_lattice(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, uint8_t* pre, uint64_t n,
+                          uint32_t* rec, uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks,
+                          uint64_t* bitmap, bool force_full, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (n > 0xffffffffull) return hipErrorInvalidValue;  // deferred indices are 32-bit
   // counters and the bitmap the curve kernel ORs into are reset here, so that
@@ -294,7 +336,7 @@ hipError_t launch_lattice(const uint8_t* sig, const uint32_t* dig, const uint8_t
   if (e == hipSuccess) e = hipMemsetAsync(tasks, 0, sizeof(unsigned long long), s);
   if (e == hipSuccess) e = hipMemsetAsync(bitmap, 0, ((n + 63) / 64) * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lattice, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sig, dig, pre, n, rec, dlist,
+  hipLaunchKernelGGL(k_lattice, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, pk, sig, dig, pre, n, rec, dlist,
                      dcount, force_full ? 1 : 0);
   return hipGetLastError();
 }

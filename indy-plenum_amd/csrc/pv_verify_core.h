@@ -197,18 +197,12 @@ PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[MSG_Y], const uint8_t* 
 
 // block `blk` of R || A || M as 16 big-endian 64-bit words from the raw message
 // words of hram_q(blk) (R, A read from sig/pk on block 0; length words on the last)
-PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[MSG_Y], const uint8_t* sig, const uint8_t* pk,
-                         const uint8_t* m, uint64_t mlen, uint64_t blk, uint64_t nblk) {
+// R || A as 16 LE words (block 0's prefix), loaded ahead by the caller
+PV_HD void hram_assemble_ra(uint64_t w[16], const uint32_t y[MSG_Y], const uint32_t ra[16], const uint8_t* m,
+                            uint64_t mlen, uint64_t blk, uint64_t nblk) {
   const bool first = blk == 0, last = blk + 1 == nblk;
   uint32_t x[32];
   msg_assemble(x, y, m, mlen, hram_q(blk));
-  uint32_t ra[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) ra[j] = 0;
-  if (first) {
-    load8(ra, sig);
-    load8(ra + 8, pk);
-  }
   // per-word bitwise selects at static indices: a `?:` between two elements
   // of x is folded by the compiler into ONE load at a computed index, which
   // forces x into private memory (scratch) -- the opaque bit-select keeps the
@@ -221,6 +215,18 @@ PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[MSG_Y], const uint8_t*
   }
   w[14] = last ? 0 : w[14];
   w[15] = last ? (64 + mlen) * 8 : w[15];
+}
+
+PV_HD void hram_assemble(uint64_t w[16], const uint32_t y[MSG_Y], const uint8_t* sig, const uint8_t* pk,
+                         const uint8_t* m, uint64_t mlen, uint64_t blk, uint64_t nblk) {
+  uint32_t ra[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) ra[j] = 0;
+  if (blk == 0) {
+    load8(ra, sig);
+    load8(ra + 8, pk);
+  }
+  hram_assemble_ra(w, y, ra, m, mlen, blk, nblk);
 }
 
 PV_HD void hram_block(uint64_t w[16], const uint8_t* sig, const uint8_t* pk, const uint8_t* m, uint64_t mlen,
