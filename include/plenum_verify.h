@@ -240,6 +240,16 @@ int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *
 #define PV_CURVE_FULL 1u
 #define PV_CURVE_GROUPED 2u
 int pv_set_curve_mode(uint32_t mode);
+
+/* Latency mode of the half-size path: generic batches of at most
+ * max_signatures signatures (per device call / host-buffer chunk) run the
+ * curve stage on lane PAIRS -- one lane holds A and the low half of s'B, the
+ * other R and the high half; they add their points at the end -- so each
+ * lane's sequential chain is ~30 % shorter (one decompression, one table, half
+ * the adds): small batches, where a few waves occupy the GPU, finish sooner.
+ * Larger batches keep the one-lane-per-signature throughput kernel.  Verdicts
+ * are identical.  Default 2048, env PV_LAT_MAX at pv_init; 0 disables. */
+int pv_set_lat_max(uint64_t max_signatures);
 int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 
 /* Live kernel timing of the verify calls themselves (bench.py's timed region):

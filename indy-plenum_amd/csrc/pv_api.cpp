@@ -45,6 +45,9 @@ int fail(int code, const char* fmt, ...) {
 // PV_HOST_CHUNKS chunks of at least PV_HOST_CHUNK_MIN signatures
 #define PV_HOST_CHUNKS 8
 #define PV_HOST_CHUNK_MIN 32768
+// generic batches of at most this many signatures run the latency-mode curve
+// kernel (lane pairs per signature); PV_LAT_MAX env overrides (0 disables)
+#define PV_LAT_MAX 2048
 // shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
 #define PV_DEDUP_SAMPLE_MIN 262144
 // chunk gathers into the pinned staging ring use up to this many host threads
@@ -305,6 +308,7 @@ struct Device {
   int copy_threads = PV_HOST_COPY_THREADS;
   int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
   size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
+  uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use k_curve_lat; PV_LAT_MAX env (0 = off)
   PinBuf pin[2];
   std::shared_ptr<GatherPool> pool = std::make_shared<GatherPool>();  // host gather threads
   PinBuf vout;  // page-locked verdicts of the shard (D2H target; copied to the caller after the drain)
@@ -374,6 +378,11 @@ int init_device(Device& d) {
   if (const char* t = getenv("PV_HOST_CHUNKS")) {
     d.host_chunks = atoi(t);
     if (d.host_chunks < 1 || d.host_chunks > 256) return fail(PV_EINVAL, "PV_HOST_CHUNKS must be in 1..256 (got %s)", t);
+  }
+  if (const char* t = getenv("PV_LAT_MAX")) {
+    const long v = atol(t);
+    if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_MAX must be in 0..1048576 (got %s)", t);
+    d.lat_max = (uint64_t)v;
   }
   if (const char* t = getenv("PV_HOST_PIN_MAX_MB")) {
     const long mb = atol(t);
@@ -503,7 +512,15 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     HIP_OK(pv::launch_lattice(pk, sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
                               d.mode == CurveMode::Full, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
-  if (half) {
+  if (half && n <= d.lat_max) {
+    // small batch: lane pairs per signature (shorter per-lane chain), one
+    // table of scratch per lane
+    HIP_OK(w.scratch.ensure(std::max<size_t>(d.scratch_words, (size_t)((2 * n + 63) / 64 * 64) * pv::ATAB_LAT_WORDS)));
+    HIP_OK(pv::launch_curve_lat(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
+                                w.scratch.cap / pv::ATAB_LAT_WORDS, verdict, bm, n, s));
+    w.half_ran = true;
+    d.last_ws = (int)(&w - d.ws);
+  } else if (half) {
     HIP_OK(pv::launch_curve_half(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
                                  w.scratch.cap / pv::HALF_SCRATCH_WORDS, verdict, bm, n, w.dlist.p, w.qc.p, w.qc.p + 1,
                                  d.curve_half_blocks, s));
@@ -926,6 +943,14 @@ int pv_set_curve_mode(uint32_t mode) {
     d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
     d.ws[0].half_ran = d.ws[1].half_ran = false;
   }
+  return PV_OK;
+}
+
+int pv_set_lat_max(uint64_t max_signatures) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (max_signatures > (1ull << 20)) return fail(PV_EINVAL, "max_signatures must be <= 2^20");
+  for (auto& d : g_devs) d.lat_max = max_signatures;
   return PV_OK;
 }
 

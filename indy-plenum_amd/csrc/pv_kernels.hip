@@ -33,6 +33,7 @@ namespace pv {
 #endif
 
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
+                  AT_WORDS == ATAB_LAT_WORDS &&
                   KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && BT_CHUNKS == BTAB_CHUNKS &&
                   HREC_WORDS == HSREC_WORDS && HALF_LANE_WORDS == HALF_SCRATCH_WORDS &&
                   BW_ENTRIES == BWTAB_ENTRIES,
@@ -247,10 +248,13 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
 __global__ __launch_bounds__(256) void k_lattice(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
                                                   const uint32_t* __restrict__ dig, uint8_t* __restrict__ pre, uint64_t n,
                                                   uint32_t* __restrict__ rec, uint32_t* __restrict__ dlist,
-                                                  unsigned long long* __restrict__ dcount, int force_full) {
+                                                  unsigned long long* __restrict__ dcount,
+                                                  unsigned long long* __restrict__ bitmap, int force_full) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   uint32_t st = HS_NONE;
   if (i < n) {
+    // the verdict bitmap the curve kernel ORs into (one word per 64 signatures)
+    if ((i & 63) == 0) bitmap[i >> 6] = 0;
     // libsodium's pre-checks (App. C.2 steps 1-3) here, one lane per
     // signature: k_hash hashed every message of the half-size path
     const bool ok = precheck(pk + 32 * i, sig + 64 * i);
@@ -320,6 +324,77 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
   }
 }
 
+// k_curve_lat: half-size verdicts of a SMALL batch on lane pairs (latency
+// mode; pv_verify_core.h side_point / msm_side): signature i runs on lanes 2i
+// (side 0: +-A and s'_lo B) and 2i + 1 (side 1: -R and s'_hi 2^128 B); side 1's
+// point reaches side 0 through a lane shuffle, side 0 adds and tests for the
+// identity.  Deferred records take the full-length verdict on side 0.  Each
+// lane's chain is one decompression, one table and 33 + 8 adds around the 128
+// doublings instead of k_curve_half's two, two and 66 + 16: batches of a few
+// waves (one per SIMD) finish sooner.  Per-lane scratch: one table (AT_WORDS).
+// The bitmap is zeroed before the launch (k_lattice) and ORed into here.
+__global__ __launch_bounds__(64) void k_curve_lat(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                                  const uint32_t* __restrict__ dig, const uint32_t* __restrict__ rec,
+                                                  const uint32_t* __restrict__ btab, const uint32_t* __restrict__ bw,
+                                                  uint32_t* __restrict__ scratch, uint8_t* __restrict__ verdict,
+                                                  unsigned long long* __restrict__ bitmap, uint64_t n) {
+  const uint64_t gl = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint64_t i = gl >> 1;
+  const int side = (int)(gl & 1);
+  uint32_t* scr = scratch + gl * AT_WORDS;
+  const uint32_t st = i < n ? (rec[HREC_WORDS * i + HREC_FLAGS] & 0xffu) : HS_NONE;
+  bool ok = false;
+  ge_p3 Q;
+  ge_p3_0(Q);
+  if (st == HS_HALF) {
+    const uint32_t* r = rec + HREC_WORDS * i;
+    ok = side_point(Q, pk + 32 * i, sig + 64 * i, r, side);
+    if (ok) {
+      build_atab(scr, Q);
+      ge_p1p1 t;
+      msm_side(t, r, scr, side ? bw + 4 * BW_TABLE : bw, side);
+      ge_p1p1_to_p3(Q, t);
+    }
+  }
+  // side 1 -> side 0 (every lane shuffles: the exchange is convergent)
+  ge_p3 Q1;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    Q1.X.v[k] = __shfl_xor(Q.X.v[k], 1, 64);
+    Q1.Y.v[k] = __shfl_xor(Q.Y.v[k], 1, 64);
+    Q1.Z.v[k] = __shfl_xor(Q.Z.v[k], 1, 64);
+    Q1.T.v[k] = __shfl_xor(Q.T.v[k], 1, 64);
+  }
+  const bool ok1 = __shfl_xor(ok ? 1 : 0, 1, 64) != 0;
+  if (side == 0 && i < n) {
+    bool v = false;
+    if (st == HS_HALF) {
+      if (ok && ok1) {
+        ge_cached c;
+        ge_p3_to_cached(c, Q1);
+        ge_p1p1 t;
+        ge_add_cached(t, Q, c, false);
+        v = p1p1_is_identity(t);
+      }
+    } else if (st == HS_DEFER) {
+      v = verify_full_one(pk + 32 * i, sig + 64 * i, dig + 16 * i, scr, btab);
+    }
+    verdict[i] = v ? 1 : 0;
+    if (v) atomicOr(&bitmap[i >> 6], 1ull << (i & 63));
+  }
+}
+
+hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, const uint32_t* rec,
+                            const uint32_t* btab, const uint32_t* bw, uint32_t* scratch, uint64_t scratch_lanes,
+                            uint8_t* verdict, uint64_t* bitmap, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (2 * n + 63) / 64;
+  if (blocks * 64 > scratch_lanes) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_curve_lat, dim3((uint32_t)blocks), dim3(64), 0, s, pk, sig, dig, rec, btab, bw, scratch,
+                     verdict, reinterpret_cast<unsigned long long*>(bitmap), n);
+  return hipGetLastError();
+}
+
 hipError_t curve_half_occupancy(int* blocks_per_cu) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_curve_half),
                                                       CURVE_BLOCK, 0);
@@ -330,14 +405,15 @@ hipError_t launch_lattice(const uint8_t* pk, const uint8_t* sig, const uint32_t*
                           uint64_t* bitmap, bool force_full, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (n > 0xffffffffull) return hipErrorInvalidValue;  // deferred indices are 32-bit
-  // counters and the bitmap the curve kernel ORs into are reset here, so that
-  // the curve launch is a single kernel (its HIP-event time == rocprof's)
-  hipError_t e = hipMemsetAsync(dcount, 0, sizeof(unsigned long long), s);
-  if (e == hipSuccess) e = hipMemsetAsync(tasks, 0, sizeof(unsigned long long), s);
-  if (e == hipSuccess) e = hipMemsetAsync(bitmap, 0, ((n + 63) / 64) * sizeof(uint64_t), s);
+  // the counters (one memset when adjacent) and the bitmap the curve kernel
+  // ORs into (zeroed by k_lattice itself) are reset here, so that the curve
+  // launch is a single kernel (its HIP-event time == rocprof's)
+  hipError_t e = tasks == dcount + 1 ? hipMemsetAsync(dcount, 0, 2 * sizeof(unsigned long long), s)
+                                     : hipMemsetAsync(dcount, 0, sizeof(unsigned long long), s);
+  if (e == hipSuccess && tasks != dcount + 1) e = hipMemsetAsync(tasks, 0, sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_lattice, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, pk, sig, dig, pre, n, rec, dlist,
-                     dcount, force_full ? 1 : 0);
+                     dcount, reinterpret_cast<unsigned long long*>(bitmap), force_full ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -1108,6 +1108,95 @@ PV_HD bool curve_half(const uint8_t* pk, const uint8_t* sig, const uint32_t* rec
   return p1p1_is_identity(t);
 }
 
+// ------------------------------------------------ latency mode (small batches)
+// One signature on a lane PAIR (k_curve_lat): side 0 holds -A (+A when c < 0)
+// and computes Q0 = |c| (+-A) + s'_lo B, side 1 holds -R and computes
+// Q1 = d (-R) + s'_hi (2^128 B) -- each over its own 9-entry table and the
+// same 33 radix-16 windows as msm_half -- and the pair then tests Q0 + Q1 == O.
+// It is msm_half's sum regrouped, so the verdict is identical; the chain one
+// lane runs shrinks from two decompressions, two tables and 66 + 16 adds to
+// one decompression, one table and 33 + 8 adds (the 128 doublings remain).
+
+// -A / +A (side 0, c's sign from the record) or -R (side 1, canonical y
+// required); false = rejected
+PV_HD bool side_point(ge_p3& P, const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, int side) {
+  uint32_t e[8];
+  load8(e, side ? sig : pk);
+  bool ok = side ? y_is_canonical(e) : true;
+  ok = ok && ge_frombytes_negate(P, e);
+  const bool flip = side == 0 && (rec[HREC_FLAGS] & 0x100u);  // c < 0: c (-A) = |c| A
+  fe u;
+  fe_neg(u, P.X);
+  fe_carry(u);
+  fe_cmov(P.X, P.X, u, flip);
+  fe_neg(u, P.T);
+  fe_carry(u);
+  fe_cmov(P.T, P.T, u, flip);
+  return ok;
+}
+
+// Horner over this side's digits: 33 windows of 4 doublings, one add from the
+// lane's table per window, and on every fourth window one affine add with the
+// side's 16-bit digit of s' (low half from the table of B, high half from
+// 2^128 B).  Leaves the last sum in p1p1 form (same window schedule as msm_half).
+template <int LS = 1>
+PV_HD void msm_side(ge_p1p1& t, const uint32_t* rec, const uint32_t* tab, const uint32_t* bt, int side) {
+  uint32_t dp[4], sp[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    dp[k] = side ? rec[HREC_D + k] : rec[HREC_C + k];
+    sp[k] = rec[HREC_S + 4 * side + k];
+  }
+  ge_p3 acc;
+  ge_p2 r2;
+  ge_p3_0(acc);
+  {
+    const int d0 = (int)((side ? rec[HREC_D + 4] : rec[HREC_C + 4]) & 15u) - 8;
+    ge_add_cached_at<LS>(t, acc, tab + (d0 < 0 ? -d0 : d0) * AT_ENTRY * LS, d0 < 0);
+    ge_p1p1_to_p2(r2, t);
+  }
+  uint32_t dw = dp[3], sw = sp[3];
+  ge_entry ea;
+  int dA = (int)((dw >> 28) & 15u) - 8;
+  load_entry<LS>(ea, tab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
+#pragma unroll 1
+  for (int w = 31; w >= 0; --w) {
+    if ((w & 7) == 7 && w != 31) {
+#pragma unroll
+      for (int k = 3; k > 0; --k) {
+        dp[k] = dp[k - 1];
+        sp[k] = sp[k - 1];
+      }
+      dw = dp[3];
+      sw = sp[3];
+    }
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+      ge_p2_dbl(t, r2);
+      ge_p1p1_to_p2(r2, t);
+    }
+    ge_p2_dbl(t, r2);
+    ge_p1p1_to_p3(acc, t);
+    const bool bwin = (w & 3) == 0;
+    const int sh16 = 16 * ((w >> 2) & 1);
+    const int dB = (int)((sw >> sh16) & 0xffffu) - 32768;
+    ge_nentry eb;
+    if (bwin) load_nentry(eb, bt + (dB < 0 ? -dB : dB) * BT_WORDS, dB < 0);
+    ge_add_entry(t, acc, ea, dA < 0);
+    if (bwin) {
+      ge_p1p1_to_p3(acc, t);
+      ge_madd_entry(t, acc, eb, dB < 0);
+    }
+    if (w == 0) break;
+    {
+      const uint32_t nw = ((w - 1) & 7) == 7 ? dp[2] : dw;
+      dA = (int)((nw >> (4 * ((w - 1) & 7))) & 15u) - 8;
+      load_entry<LS>(ea, tab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
+    }
+    ge_p1p1_to_p2(r2, t);
+  }
+}
+
 // Full-length verdict of one signature (deferred records): R' = h(-A) + S B,
 // encode, compare.  scratch = AT_WORDS words (stride LS); btab = table of B.
 template <int LS = 1>

@@ -59,6 +59,7 @@ SIGNATURES = [
       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ('pv_curve_stats', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)]),
     ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
+    ('pv_set_lat_max', ctypes.c_int, [ctypes.c_uint64]),
     ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
     ('pv_kernel_timing', ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
@@ -81,6 +82,15 @@ def set_curve_mode(name):
     """Curve-stage schedule of generic batches on every initialised device (pv_set_curve_mode)."""
     code = {v: k for k, v in CURVE_MODES.items()}[name]
     _check('pv_set_curve_mode', load().pv_set_curve_mode(code))
+
+
+LAT_MAX_DEFAULT = 2048   # PV_LAT_MAX in csrc/pv_api.cpp
+
+
+def set_lat_max(max_signatures):
+    """Largest generic batch that runs the latency-mode curve kernel (lane pairs
+    per signature) on every initialised device; 0 disables (pv_set_lat_max)."""
+    _check('pv_set_lat_max', load().pv_set_lat_max(int(max_signatures)))
 
 
 STAGING_MODES = {0: 'pinned', 1: 'pageable'}   # PV_STAGING_PINNED / _PAGEABLE

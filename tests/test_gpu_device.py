@@ -66,9 +66,11 @@ def test_c2_full_size_properties(torch_dev):
 
 
 def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
-    """The half-size path (default), every record through its full-length
-    tasks (PV_CURVE_MODE=full) and the grouped kernel give identical verdicts
-    and bitmaps; the half path's deferred records really ran (C2-shaped batch)."""
+    """The half-size path (default; throughput kernel and the latency-mode
+    lane-pair kernel), every record through its full-length tasks
+    (PV_CURVE_MODE=full) and the grouped kernel give identical verdicts and
+    bitmaps on a 200k C2-shaped batch and on every fixture; the half path's
+    deferred records really ran."""
     from plenum_gpu import _native as nat
     from plenum_gpu.device import SyntheticBatch
     from plenum_gpu.nacl_wrappers import verify_signed_batch
@@ -79,7 +81,11 @@ def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
     rows = split_sm(adversarial)
     r = raw_vectors
     try:
-        for mode in ('half', 'full', 'grouped'):
+        for mode in ('half', 'half_lat', 'full', 'grouped'):
+            # half: one lane per signature everywhere; half_lat: lane pairs for
+            # the 200k batch and every fixture
+            nat.set_lat_max(1 << 20 if mode == 'half_lat' else 0)
+            mode = 'half' if mode == 'half_lat' else mode
             nat.set_curve_mode(mode)
             b.bitmap.fill_(-1)     # the half path must clear it itself
             v = b.verify().cpu().numpy().astype(bool)
@@ -99,6 +105,7 @@ def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
             assert not wrong, (mode, wrong)
     finally:
         nat.set_curve_mode('half')
+        nat.set_lat_max(nat.LAT_MAX_DEFAULT)
 
 
 def test_kernel_timer(torch_dev):
