@@ -440,6 +440,9 @@ def main():
     ap.add_argument('--no-e2e', action='store_true', help='skip the host-buffer (PCIe-inclusive) measurement')
     ap.add_argument('--no-key-cache', action='store_true',
                     help='c3/c4: re-decompress every key per signature instead of preparing each distinct key once')
+    ap.add_argument('--sequential', action='store_true',
+                    help='one stream, each step after the previous one (default: consecutive steps alternate over '
+                         'two streams and two workspaces, so step k + 1 starts while step k\'s curve grid drains)')
     args = ap.parse_args()
     if args.config == 'c1':
         return main_c1(args)
@@ -482,26 +485,47 @@ def main():
     batch = SyntheticBatch(local, n, cfg['mlen'], cfg=cfg['cfg'], first=rank * n, key_mod=cfg['key_mod'],
                            mode=cfg['mode'], mlen_max=cfg['mlen_max'], n_nodes=n_nodes)
     key_cache = batch.use_key_cache(not args.no_key_cache)   # keys repeat in c3 (node keys) and c4 (key pool)
+    batch.make_slots()
     torch.cuda.synchronize()
-    gathered = torch.zeros(world * batch.bitmap.numel(), dtype=torch.int64, device=dev) if world > 1 else None
+    pipelined = not args.sequential
+    # pipelined steps: step k runs on stream k % 2 with verify workspace and
+    # outputs k % 2 (pv_*_async), so step k + 1's hash and curve grids start on
+    # CUs that step k's curve grid has finished with; a slot is reused two
+    # steps later on the same stream (ordered)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)] if pipelined else None
+    slots = 2 if pipelined else 1
+    gathered = [torch.zeros(world * batch.bitmap.numel(), dtype=torch.int64, device=dev)
+                for _ in range(slots)] if world > 1 else None
     tally = None
     if cfg['mode'] == synth.COMMIT:
         nb = n // n_nodes
         q = Quorums(n_nodes).commit.value
         tally = dict(nb=nb, q=q, boff=torch.arange(nb + 1, dtype=torch.int64, device=dev) * n_nodes,
-                     votes=torch.empty(nb, dtype=torch.int32, device=dev),
-                     reached=torch.empty(nb, dtype=torch.uint8, device=dev),
-                     gathered=torch.empty(world * nb, dtype=torch.uint8, device=dev))
+                     votes=[torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(slots)],
+                     reached=[torch.empty(nb, dtype=torch.uint8, device=dev) for _ in range(slots)],
+                     gathered=[torch.empty(world * nb, dtype=torch.uint8, device=dev) for _ in range(slots)])
+
+    def finish(slot, verdict, bitmap):
+        if tally is not None:
+            tally_device(verdict, batch.sender, tally['boff'], n_nodes, tally['q'], tally['votes'][slot],
+                         tally['reached'][slot])
+        if world > 1:
+            all_gather(gathered[slot], bitmap)
+            if tally is not None:   # C3: batch-sharded tallies, gather the quorum bits
+                all_gather(tally['gathered'][slot], tally['reached'][slot])
+
+    counter = [0]
 
     def step():
-        batch.verify()
-        if tally is not None:
-            tally_device(batch.verdict, batch.sender, tally['boff'], n_nodes, tally['q'], tally['votes'],
-                         tally['reached'])
-        if world > 1:
-            all_gather(gathered, batch.bitmap)
-            if tally is not None:   # C3: batch-sharded tallies, gather the quorum bits
-                all_gather(tally['gathered'], tally['reached'])
+        if not pipelined:
+            batch.verify()
+            finish(0, batch.verdict, batch.bitmap)
+            return
+        slot = counter[0] & 1
+        counter[0] += 1
+        with torch.cuda.stream(streams[slot]):
+            verdict, bitmap = batch.verify_async(slot, streams[slot])
+            finish(slot, verdict, bitmap)
 
     for _ in range(args.warmup):
         step()
@@ -509,7 +533,10 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    nat.kernel_timing(local, True)   # HIP events around each verify launch of the timed steps
+    # HIP events around each verify launch of the timed steps (sequential
+    # schedule); pipelined launches overlap, so their kernels are timed on
+    # sequential calibration steps after the timed region instead
+    nat.kernel_timing(local, not pipelined)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -523,33 +550,39 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # correctness of the measured pass: verdict == not tampered, bitmap == verdict
-    verdict = batch.verdict.cpu().numpy().astype(bool)
+    # correctness of the measured passes (every output slot): verdict == not
+    # tampered, bitmap == verdict, quorum bits == the spec's
     tamper = batch.tamper.cpu().numpy().astype(bool)
-    mism = int((verdict == tamper).sum())
-    bits = np.unpackbits(batch.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
-    mism += int((bits != verdict).sum())
-    if tally is not None:
-        want_votes, want_reached = synth.c3_expected(rank * tally['nb'], tally['nb'], n_nodes, tally['q'])
-        mism += int((tally['votes'].cpu().numpy() != want_votes.astype(np.int32)).sum())
-        mism += int((tally['reached'].cpu().numpy().astype(bool) != want_reached).sum())
+    mism = 0
+    used = min(slots, args.steps + args.warmup)
+    for slot in range(used):
+        v_t, b_t, _ = batch.slot_out[slot]
+        verdict = v_t.cpu().numpy().astype(bool)
+        mism += int((verdict == tamper).sum())
+        bits = np.unpackbits(b_t.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
+        mism += int((bits != verdict).sum())
+        if tally is not None:
+            want_votes, want_reached = synth.c3_expected(rank * tally['nb'], tally['nb'], n_nodes, tally['q'])
+            mism += int((tally['votes'][slot].cpu().numpy() != want_votes.astype(np.int32)).sum())
+            mism += int((tally['reached'][slot].cpu().numpy().astype(bool) != want_reached).sum())
+            if world > 1:
+                _, all_reached = synth.c3_expected(0, world * tally['nb'], n_nodes, tally['q'])
+                mism += int((tally['gathered'][slot].cpu().numpy().astype(bool) != all_reached).sum())
         if world > 1:
-            _, all_reached = synth.c3_expected(0, world * tally['nb'], n_nodes, tally['q'])
-            mism += int((tally['gathered'].cpu().numpy().astype(bool) != all_reached).sum())
+            # own slice of the gathered bitmaps == own verdicts, and every rank holds
+            # the same gathered bytes (checksums equal under MIN and MAX)
+            g = gathered[slot].cpu().numpy()
+            allbits = np.unpackbits(g.view(np.uint8), bitorder='little')
+            per = batch.bitmap.numel() * 64
+            mine = allbits[rank * per: rank * per + n].astype(bool)
+            mism += int((mine != verdict).sum())
+            import hashlib
+            ck = int.from_bytes(hashlib.sha256(g.tobytes()).digest()[:7], 'little')
+            cks = [coll_dev(torch.tensor([ck], dtype=torch.int64, device=dev)) for _ in range(2)]
+            dist.all_reduce(cks[0], op=dist.ReduceOp.MIN)
+            dist.all_reduce(cks[1], op=dist.ReduceOp.MAX)
+            mism += int(cks[0].item() != cks[1].item())
     if world > 1:
-        # own slice of the gathered bitmaps == own verdicts, and every rank holds
-        # the same gathered bytes (checksums equal under MIN and MAX)
-        g = gathered.cpu().numpy()
-        allbits = np.unpackbits(g.view(np.uint8), bitorder='little')
-        per = batch.bitmap.numel() * 64
-        mine = allbits[rank * per: rank * per + n].astype(bool)
-        mism += int((mine != verdict).sum())
-        import hashlib
-        ck = int.from_bytes(hashlib.sha256(g.tobytes()).digest()[:7], 'little')
-        cks = [coll_dev(torch.tensor([ck], dtype=torch.int64, device=dev)) for _ in range(2)]
-        dist.all_reduce(cks[0], op=dist.ReduceOp.MIN)
-        dist.all_reduce(cks[1], op=dist.ReduceOp.MAX)
-        mism += int(cks[0].item() != cks[1].item())
         m = coll_dev(torch.tensor([mism], dtype=torch.int64, device=dev))
         dist.all_reduce(m)
         mism = int(m.item())
@@ -557,6 +590,16 @@ def main():
     # kernel-level timing for the roofline: HIP events on the launch stream,
     # recorded during the timed steps above (averaged over those launches)
     h_sum, c_sum, launches = nat.kernel_timing(local, False)
+    calib = 0
+    if pipelined:
+        # kernel durations on their own: a few steps, one after the other, with
+        # HIP events on the launch stream (outside the timed region)
+        calib = 3
+        nat.kernel_timing(local, True)
+        for _ in range(calib):
+            batch.verify()
+        torch.cuda.synchronize()
+        h_sum, c_sum, launches = nat.kernel_timing(local, False)
     ms_hash, ms_curve = h_sum / max(1, launches), c_sum / max(1, launches)
     curve_mode, deferred = nat.curve_stats(local)
     if key_cache:
@@ -571,7 +614,12 @@ def main():
         wpv = {'fe_mul': W_MUL_PER_VERIFY, 'fe_sq': W_SQ_PER_VERIFY, 'mad': W_MAD_PER_VERIFY,
                'deferred_full_length': {'count': deferred, 'fe_mul': W_MUL_FULL, 'fe_sq': W_SQ_FULL,
                                         'mad': W_MAD_FULL}}
-    achieved = work / (ms_curve * 1e-3)
+    ms_step = elapsed / args.steps * 1e3
+    # pipelined: the dominant kernel is priced on the per-step time of the timed
+    # region (every kernel of the step charged to it: a lower bound on its own
+    # rate); sequential: on its HIP-event duration in the timed steps
+    achieved = work / ((ms_step if pipelined else ms_curve) * 1e-3)
+    achieved_events = work / (ms_curve * 1e-3)
     peak = _mad_peak()
 
     total = world * n * args.steps
@@ -591,20 +639,30 @@ def main():
                        world, 'RCCL' if backend == 'nccl' else backend + ' (rehearsal, ranks share GPU 0)')
                    if world > 1 else 'single GPU'},
         'verdict_mismatches': mism,
-        'kernel_ms': {'hash': round(ms_hash, 4), 'curve': round(ms_curve, 4)},
+        'kernel_ms': {'hash': round(ms_hash, 4), 'curve': round(ms_curve, 4),
+                      'timed_on': '{} sequential calibration steps after the timed region'.format(calib)
+                      if pipelined else 'the timed steps'},
         'roofline': {'bound': 'valu', 'kernel': kernel,
                      'achieved': round(achieved / 1e12, 3), 'peak': round(peak / 1e12, 3),
                      'unit': 'Tmad/s (v_mad_u64_u32 lane-ops)', 'frac': round(achieved / peak, 4),
+                     'timing': 'curve MAD work per step / per-step time of the timed region (pipelined steps '
+                               'overlap; hash + lattice charged to the curve kernel too)' if pipelined else
+                               'curve MAD work / HIP-event duration of the curve launch in the timed steps',
+                     'kernel_events': {'curve_ms': round(ms_curve, 4), 'achieved': round(achieved_events / 1e12, 3),
+                                       'frac': round(achieved_events / peak, 4)},
                      'traffic': _traffic_per_launch() if (args.config, n) == ('c2', CONFIGS['c2']['n']) else None,
                      'work_per_verify': wpv},
         'curve_mode': curve_mode if not key_cache else 'keyed',
+        'schedule': 'pipelined: consecutive steps alternate over 2 streams + 2 verify workspaces/output sets '
+                    '(step k + 1 starts while step k drains; all K steps complete inside the timed region)'
+                    if pipelined else 'sequential: one stream',
         'cpu_baseline': None,
     }
     if tally is not None:
         out['config']['batches_per_gpu'] = tally['nb']
         out['config']['quorum'] = tally['q']
         out['batches_per_s'] = round(world * tally['nb'] * args.steps / elapsed, 1)
-        out['quorum_reached'] = int(tally['reached'].sum().item())
+        out['quorum_reached'] = int(tally['reached'][0].sum().item())
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(batch, args.config.upper())
     if world == 1 and args.config == 'c2' and not args.no_e2e:

@@ -110,6 +110,24 @@ int pv_verify_batch(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_bl
 int pv_verify_batch_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off,
                            uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device, void *stream);
 
+/* Enqueue-only forms for pipelined device callers: the work is queued on
+ * `stream` (NULL = the library stream of `slot`) with verify workspace `slot`
+ * (0 or 1) and the call returns without waiting; the caller synchronises its
+ * stream.  Two batches in flight at once must use different slots and
+ * different output buffers (verdict, bitmap; for keys, ktab); work reusing a
+ * slot must be ordered after that slot's previous batch (same stream, or an
+ * event).  Inputs must be ready on `stream` (the caller orders its own writes).
+ * A caller alternating two streams and two slots over consecutive batches lets
+ * batch k + 1's hash stage run while batch k's curve grid drains.  bitmap is
+ * required here. */
+int pv_verify_batch_device_async(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_blob,
+                                 const uint64_t *msg_off, uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device,
+                                 void *stream, int slot);
+int pv_verify_keyed_device_async(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk, const uint8_t *sig,
+                                 const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n, uint8_t *verdict,
+                                 uint64_t *bitmap, int device, void *stream, int slot);
+int pv_keys_prepare_device_async(const uint8_t *pk, uint64_t k, uint32_t *ktab, int device, void *stream, int slot);
+
 /* Verifying-key cache on the device.  pv_keys_prepare_device fills ktab
  * (k x PV_KEY_WORDS words) for the k 32-byte keys in pk; a key that libsodium
  * would refuse (non-canonical, small order, not on the curve) is marked so and
@@ -254,8 +272,10 @@ int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 
 /* Live kernel timing of the verify calls themselves (bench.py's timed region):
  * enable = 1 resets and starts recording HIP events around the hash and curve
- * stages of every verify launch on `device` (on the launch stream); enable = 0
- * stops and returns the summed milliseconds and the number of launches. */
+ * stages of every verify launch on `device` (on the launch stream, without
+ * waiting for them: async launches stay in flight); enable = 0 stops, waits
+ * for the recorded events and returns the summed milliseconds and the number
+ * of launches. */
 int pv_kernel_timing(int device, int enable, float *hash_ms, float *curve_ms, uint64_t *launches);
 
 /* pv_time_verify_device for keyed batches. */

@@ -331,7 +331,7 @@ struct Device {
   DevBuf<uint8_t> reached;
   DevBuf<uint64_t> scan;      // block sums of the device prefix scan
   DevBuf<uint32_t> ktab, kidx;  // prepared keys + per-signature key index (deduplicated host batches)
-  DevBuf<uint32_t> kscr;        // key-preparation scratch
+  DevBuf<uint32_t> kscr, kscr2;  // key-preparation scratch (kscr2: async slot 1)
   DevBuf<uint32_t> mk0, mk1;    // Merkle level ping-pong / leaf digests
   int sha256_blocks = 0;
   int curve_blocks_keyed = 0;
@@ -341,6 +341,14 @@ struct Device {
   bool live_timing = false;
   float live_hash = 0, live_curve = 0;
   uint64_t live_launches = 0;
+  // live timing records three events per launch without waiting (pipelined
+  // callers keep launches in flight); they are resolved when the pool fills
+  // up and when timing stops
+  struct LiveRec {
+    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  };
+  std::vector<LiveRec> live_pool;
+  size_t live_used = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -455,9 +463,14 @@ void release_device(Device& d) {
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release(); d.tflag.release(); d.tbits.release();
-  d.ktab.release(); d.kidx.release(); d.kscr.release(); d.mk0.release(); d.mk1.release();
+  d.ktab.release(); d.kidx.release(); d.kscr.release(); d.kscr2.release(); d.mk0.release(); d.mk1.release();
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
+  for (auto& r : d.live_pool)
+    for (auto& e : r.e)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+  d.live_pool.clear();
+  d.live_used = 0;
   if (d.copied) (void)hipEventDestroy(d.copied);
   d.copied = nullptr;
   if (d.copy) (void)hipStreamSynchronize(d.copy), (void)hipStreamDestroy(d.copy);
@@ -475,16 +488,38 @@ void release_device(Device& d) {
   d.id = -1;
 }
 
+// fold the recorded live-timing events into the sums (waits for them)
+int resolve_live(Device& d) {
+  for (size_t k = 0; k < d.live_used; ++k) {
+    hipEvent_t* e = d.live_pool[k].e;
+    HIP_OK(hipEventSynchronize(e[2]));
+    float a = 0, b = 0;
+    HIP_OK(hipEventElapsedTime(&a, e[0], e[1]));
+    HIP_OK(hipEventElapsedTime(&b, e[1], e[2]));
+    d.live_hash += a;
+    d.live_curve += b;
+  }
+  d.live_used = 0;
+  return PV_OK;
+}
+
 // enqueue hash + curve for device-resident inputs on stream s with workspace w
 int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                    const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed,
                    float* ms_hash, float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
   if (n == 0) return PV_OK;
   const bool live = !timed && d.live_timing;
+  hipEvent_t* lev = nullptr;
   if (live) {
-    timed = true;
-    ms_hash = &d.live_hash;
-    ms_curve = &d.live_curve;
+    if (d.live_used == d.live_pool.size() && d.live_used >= 256) {
+      const int rc = resolve_live(d);
+      if (rc) return rc;
+    }
+    if (d.live_used == d.live_pool.size()) {
+      d.live_pool.emplace_back();
+      for (auto& e : d.live_pool.back().e) HIP_OK(hipEventCreate(&e));
+    }
+    lev = d.live_pool[d.live_used++].e;
     ++d.live_launches;
   }
   HIP_OK(w.h.ensure(n * 16));
@@ -504,6 +539,7 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     HIP_OK(w.dlist.ensure(n));
   }
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
+  if (lev) HIP_OK(hipEventRecord(lev[0], s));
   // the half-size path runs the pre-checks in k_lattice (k_hash hashes every
   // signature); keyed and grouped batches in k_precheck before the hash
   HIP_OK(pv::launch_hash(pk, sig, blob, off, n, w.counter.p, w.h.p, half ? nullptr : w.pre.p, d.hash_blocks, s, kidx));
@@ -512,6 +548,7 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     HIP_OK(pv::launch_lattice(pk, sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
                               d.mode == CurveMode::Full, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
+  if (lev) HIP_OK(hipEventRecord(lev[1], s));
   if (half && n <= d.lat_max) {
     // small batch: lane pairs per signature (shorter per-lane chain), one
     // table of scratch per lane
@@ -530,6 +567,7 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     HIP_OK(pv::launch_curve(pk, sig, w.h.p, w.pre.p, d.btab.p, w.scratch.p, w.scratch.cap / pv::ATAB_WORDS, verdict,
                             bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p));
   }
+  if (lev) HIP_OK(hipEventRecord(lev[2], s));
   if (timed) {
     HIP_OK(hipEventRecord(d.ev[2], s));
     HIP_OK(hipEventSynchronize(d.ev[2]));
@@ -846,6 +884,54 @@ int pv_verify_batch_device(const uint8_t* pk, const uint8_t* sig, const uint8_t*
   return PV_OK;
 }
 
+int pv_verify_batch_device_async(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob,
+                                 const uint64_t* msg_off, uint64_t n, uint8_t* verdict, uint64_t* bitmap, int device,
+                                 void* stream, int slot) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
+  if (n == 0) return PV_OK;
+  if (!pk || !sig || !msg_blob || !msg_off || !verdict || !bitmap) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
+  return enqueue_verify(*d, d->ws[slot], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr);
+}
+
+int pv_verify_keyed_device_async(const uint32_t* ktab, const uint32_t* key_idx, const uint8_t* pk, const uint8_t* sig,
+                                 const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n, uint8_t* verdict,
+                                 uint64_t* bitmap, int device, void* stream, int slot) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
+  if (n == 0) return PV_OK;
+  if (!ktab || !key_idx || !pk || !sig || !msg_blob || !msg_off || !verdict || !bitmap)
+    return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
+  return enqueue_verify(*d, d->ws[slot], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr,
+                        ktab, key_idx);
+}
+
+int pv_keys_prepare_device_async(const uint8_t* pk, uint64_t k, uint32_t* ktab, int device, void* stream, int slot) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
+  if (k == 0) return PV_OK;
+  if (!pk || !ktab) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
+  DevBuf<uint32_t>& scr = slot ? d->kscr2 : d->kscr;
+  HIP_OK(scr.ensure(k * pv::KEYTAB_SCRATCH));
+  HIP_OK(pv::launch_keys(pk, k, ktab, scr.p, s));
+  return PV_OK;
+}
+
 int pv_keys_prepare_device(const uint8_t* pk, uint64_t k, uint32_t* ktab, int device, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceGuard dg;
@@ -924,6 +1010,12 @@ int pv_kernel_timing(int device, int enable, float* hash_ms, float* curve_ms, ui
   std::lock_guard<std::mutex> lk(g_mu);
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  DeviceGuard dg;
+  HIP_OK(hipSetDevice(device));
+  {
+    const int rc = resolve_live(*d);
+    if (rc) return rc;
+  }
   if (enable) {
     d->live_hash = d->live_curve = 0;
     d->live_launches = 0;

@@ -20,6 +20,7 @@
 // any exact representation is parity-equivalent.
 #pragma once
 #include <stdint.h>
+#include "pv_madchains.h"
 
 #ifndef PV_HD
 #define PV_HD __host__ __device__ __forceinline__
@@ -311,6 +312,158 @@ PV_HD void fe_sq(fe& h, const fe& f) {
     out[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
   }
   fe_finish_columns(h, carry, out);
+  PV_FE_FENCE();
+}
+
+// ---- two / three independent products at once (k_curve_half's hot loop).
+// Same column sums, carries and bounds as fe_mul / fe_sq; on the device each
+// column of the C products is ONE asm block with the C v_mad_u64_u32 chains
+// interleaved instruction by instruction (pv_madchains.h), so a wave always
+// has C independent MADs to issue instead of one serial chain.
+template <int C>
+PV_HD void fe_mul_n(fe* const h[C], const fe* const f[C], const fe* const g[C]) {
+#if defined(PV_MADN_PLAIN)
+#pragma unroll
+  for (int c = 0; c < C; ++c) fe_mul(*h[c], *f[c], *g[c]);
+#else
+  uint32_t g19[C][10], f2[C][10];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    PV_COUNT(mul);
+#pragma unroll
+    for (int j = 1; j < 10; ++j) g19[c][j] = 19u * g[c]->v[j];
+#pragma unroll
+    for (int i = 1; i < 10; i += 2) f2[c][i] = 2u * f[c]->v[i];
+  }
+  uint64_t carry[C];
+  uint32_t out[C][10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    uint32_t a[C][10], b[C][10];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+        const int j = (k - i + 10) % 10;
+        const bool oo = (i & 1) && (j & 1);
+        a[c][i] = oo ? f2[c][i] : f[c]->v[i];
+        b[c][i] = i + j >= 10 ? g19[c][j] : g[c]->v[j];
+      }
+    }
+    uint64_t acc[C];
+    if constexpr (C == 2) {
+      if (k == 0) madc10x2z(acc[0], acc[1], a[0], b[0], a[1], b[1]);
+      else madc10x2(acc[0], acc[1], a[0], b[0], a[1], b[1], carry[0], carry[1]);
+    } else {
+      static_assert(C == 3, "fe_mul_n: 2 or 3 products");
+      if (k == 0) madc10x3z(acc[0], acc[1], acc[2], a[0], b[0], a[1], b[1], a[2], b[2]);
+      else madc10x3(acc[0], acc[1], acc[2], a[0], b[0], a[1], b[1], a[2], b[2], carry[0], carry[1], carry[2]);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      carry[c] = acc[c] >> ((k & 1) ? 25 : 26);
+      out[c][k] = (uint32_t)acc[c] & ((k & 1) ? M25 : M26);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) fe_finish_columns(*h[c], carry[c], out[c]);
+#endif
+}
+
+template <int C>
+PV_HD void fe_sq_n(fe* const h[C], const fe* const f[C]) {
+#if defined(PV_MADN_PLAIN)
+#pragma unroll
+  for (int c = 0; c < C; ++c) fe_sq(*h[c], *f[c]);
+#else
+  uint32_t f2[C][10], f19[C][10], f4[C][10];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    PV_COUNT(sq);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) f2[c][i] = 2u * f[c]->v[i];
+#pragma unroll
+    for (int i = 5; i < 10; ++i) f19[c][i] = 19u * f[c]->v[i];
+#pragma unroll
+    for (int i = 1; i < 10; i += 2) f4[c][i] = 4u * f[c]->v[i];
+  }
+  uint64_t carry[C];
+  uint32_t out[C][10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    uint32_t as[C][6], bs[C][6];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      int t = 0;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+#pragma unroll
+        for (int j = i; j < 10; ++j) {
+          if ((i + j) % 10 != k) continue;
+          const bool oo = (i & 1) && (j & 1);
+          const bool wrap = i + j >= 10;
+          uint32_t x, y;
+          if (i == j) {
+            if (!wrap) { x = f[c]->v[i]; y = oo ? f2[c][i] : f[c]->v[i]; }
+            else { x = oo ? f2[c][i] : f[c]->v[i]; y = f19[c][i]; }
+          } else {
+            x = oo ? f4[c][i] : f2[c][i];
+            y = wrap ? f19[c][j] : f[c]->v[j];
+          }
+          as[c][t] = x;
+          bs[c][t] = y;
+          ++t;
+        }
+      }
+    }
+    uint64_t acc[C];
+    if constexpr (C == 2) {
+      if (k & 1) madc5x2(acc[0], acc[1], as[0], bs[0], as[1], bs[1], carry[0], carry[1]);
+      else if (k == 0) madc6x2z(acc[0], acc[1], as[0], bs[0], as[1], bs[1]);
+      else madc6x2(acc[0], acc[1], as[0], bs[0], as[1], bs[1], carry[0], carry[1]);
+    } else {
+      static_assert(C == 3, "fe_sq_n: 2 or 3 squares");
+      if (k & 1) madc5x3(acc[0], acc[1], acc[2], as[0], bs[0], as[1], bs[1], as[2], bs[2], carry[0], carry[1], carry[2]);
+      else if (k == 0) madc6x3z(acc[0], acc[1], acc[2], as[0], bs[0], as[1], bs[1], as[2], bs[2]);
+      else madc6x3(acc[0], acc[1], acc[2], as[0], bs[0], as[1], bs[1], as[2], bs[2], carry[0], carry[1], carry[2]);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      carry[c] = acc[c] >> ((k & 1) ? 25 : 26);
+      out[c][k] = (uint32_t)acc[c] & ((k & 1) ? M25 : M26);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) fe_finish_columns(*h[c], carry[c], out[c]);
+#endif
+}
+
+PV_HD void fe_mul2(fe& h0, const fe& f0, const fe& g0, fe& h1, const fe& f1, const fe& g1) {
+  PV_CHECK_MUL(f0, g0);
+  PV_CHECK_MUL(f1, g1);
+  fe* const h[2] = {&h0, &h1};
+  const fe* const f[2] = {&f0, &f1};
+  const fe* const g[2] = {&g0, &g1};
+  fe_mul_n<2>(h, f, g);
+  PV_FE_FENCE();
+}
+PV_HD void fe_mul3(fe& h0, const fe& f0, const fe& g0, fe& h1, const fe& f1, const fe& g1, fe& h2, const fe& f2,
+                   const fe& g2) {
+  PV_CHECK_MUL(f0, g0);
+  PV_CHECK_MUL(f1, g1);
+  PV_CHECK_MUL(f2, g2);
+  fe* const h[3] = {&h0, &h1, &h2};
+  const fe* const f[3] = {&f0, &f1, &f2};
+  const fe* const g[3] = {&g0, &g1, &g2};
+  fe_mul_n<3>(h, f, g);
+  PV_FE_FENCE();
+}
+PV_HD void fe_sq2(fe& h0, const fe& f0, fe& h1, const fe& f1) {
+  PV_CHECK_SQ(f0);
+  PV_CHECK_SQ(f1);
+  fe* const h[2] = {&h0, &h1};
+  const fe* const f[2] = {&f0, &f1};
+  fe_sq_n<2>(h, f);
   PV_FE_FENCE();
 }
 

@@ -116,6 +116,34 @@ class SyntheticBatch:
                                               _stream(self.device)))
         return self.verdict
 
+    def make_slots(self):
+        """Output buffers for two batches in flight (pipelined steps): slot 0 is
+        (verdict, bitmap, ktab), slot 1 a second set.  Call after use_key_cache."""
+        self.slot_out = [(self.verdict, self.bitmap, self.ktab),
+                         (torch.empty_like(self.verdict), torch.zeros_like(self.bitmap),
+                          None if self.ktab is None else torch.empty_like(self.ktab))]
+
+    def verify_async(self, slot, stream):
+        """Enqueue one pass of the hot path on `stream` with workspace/output
+        `slot` (pv_*_async): returns (verdict, bitmap) of the slot without
+        waiting.  Two passes in flight must use different slots."""
+        lib = nat.load()
+        verdict, bitmap, ktab = self.slot_out[slot]
+        s = ctypes.c_void_p(stream.cuda_stream)
+        dev = self.device.index
+        if self.keys is not None:
+            upk, kidx = self.keys
+            nat._check('pv_keys_prepare_device_async',
+                       lib.pv_keys_prepare_device_async(_p(upk), upk.shape[0], _p(ktab), dev, s, slot))
+            nat._check('pv_verify_keyed_device_async',
+                       lib.pv_verify_keyed_device_async(_p(ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob),
+                                                        _p(self.off), self.n, _p(verdict), _p(bitmap), dev, s, slot))
+        else:
+            nat._check('pv_verify_batch_device_async',
+                       lib.pv_verify_batch_device_async(_p(self.pk), _p(self.sig), _p(self.blob), _p(self.off),
+                                                        self.n, _p(verdict), _p(bitmap), dev, s, slot))
+        return verdict, bitmap
+
     def time_kernels(self, iters):
         """Average (hash_ms, curve_ms) per launch from HIP events on the launch stream."""
         lib = nat.load()

@@ -247,3 +247,56 @@ def test_c4_full_shard(torch_dev):
     want = orc.verify_batch(pk, sig, np.concatenate(msgs), loff)
     assert (verdicts[0][idx] == want).all()
     assert not want.all() and want.any()
+
+
+@pytest.mark.parametrize('keyed', [False, True])
+def test_pipelined_async_slots(torch_dev, keyed):
+    """bench.py's pipelined schedule: passes alternate over two streams with
+    verify workspaces / output sets 0 and 1 (pv_*_device_async), several in
+    flight at once; every slot's verdicts and bitmap equal the synchronous
+    pass, and the generic path matches the oracle on a sample."""
+    torch = torch_dev
+    from plenum_gpu.device import SyntheticBatch
+    n = 200_000
+    b = SyntheticBatch(0, n, 128, cfg=4, mode=1, mlen_max=1024, key_mod=4096 if keyed else 0)
+    b.use_key_cache(keyed)
+    b.make_slots()
+    want = b.verify().cpu().numpy().copy()
+    want_bits = b.bitmap.cpu().numpy().copy()
+    tamper = b.tamper.cpu().numpy().astype(bool)
+    assert (want.astype(bool) == ~tamper).all()
+    for slot in range(2):
+        b.slot_out[slot][0].fill_(7)
+        b.slot_out[slot][1].zero_()
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(b.device), torch.cuda.Stream(b.device)]
+    for k in range(6):
+        with torch.cuda.stream(streams[k & 1]):
+            b.verify_async(k & 1, streams[k & 1])
+    torch.cuda.synchronize()
+    for slot in range(2):
+        v, bm, _ = b.slot_out[slot]
+        assert (v.cpu().numpy() == want).all()
+        assert (bm.cpu().numpy() == want_bits).all()
+    if not keyed:
+        idx = np.random.default_rng(1).choice(n, 200, replace=False)
+        off = b.off.cpu().numpy().astype(np.uint64)
+        blob = b.blob.cpu().numpy()
+        pk, sig = b.pk.cpu().numpy()[idx], b.sig.cpu().numpy()[idx]
+        msgs = [blob[int(off[i]):int(off[i + 1])].tobytes() for i in idx]
+        soff = np.zeros(len(idx) + 1, np.uint64)
+        soff[1:] = np.cumsum([len(m) for m in msgs])
+        got = orc.verify_batch(pk, sig, np.frombuffer(b''.join(msgs), np.uint8), soff)
+        assert (got == want[idx].astype(bool)).all()
+
+
+def test_async_slot_rejected(torch_dev):
+    """Workspace slots other than 0 and 1 are refused through the C-ABI."""
+    import ctypes
+    from plenum_gpu import _native as nat
+    from plenum_gpu.device import SyntheticBatch, _p
+    b = SyntheticBatch(0, 64, 32, cfg=2)
+    s = ctypes.c_void_p(torch_dev.cuda.current_stream(b.device).cuda_stream)
+    rc = nat.load().pv_verify_batch_device_async(_p(b.pk), _p(b.sig), _p(b.blob), _p(b.off), b.n, _p(b.verdict),
+                                                 _p(b.bitmap), 0, s, 2)
+    assert rc != 0
