@@ -62,6 +62,20 @@ struct fe {
 
 PV_HD uint64_t mul32x32(uint32_t a, uint32_t b) { return (uint64_t)a * (uint64_t)b; }
 
+// 2x of a limb.  -DPV_TWICE_ADD forces v_add_u32 (asm) instead of the
+// compiler's v_lshlrev_b32: the isolated issue rates suggest it should be
+// cheaper (profiles/r01_int_cycles.json), but the doubling chain measured 2 %
+// slower with it (profiles/r02_fe_ilp_twice.txt), so the default is the shift.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PV_FE_NOASM) && defined(PV_TWICE_ADD)
+__device__ __forceinline__ uint32_t twice(uint32_t x) {
+  uint32_t y;
+  asm("v_add_u32 %0, %1, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+#else
+PV_HD uint32_t twice(uint32_t x) { return 2u * x; }
+#endif
+
 // Column sums as v_mad_u64_u32 chains whose first addend is the incoming
 // carry.  As plain C++ the compiler reassociates every column (starts it from
 // 0 and adds the carry with a trailing v_lshl_add_u64: one extra half-rate
@@ -246,7 +260,7 @@ PV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
 #pragma unroll
   for (int j = 1; j < 10; ++j) g19[j] = 19u * g.v[j];
 #pragma unroll
-  for (int i = 1; i < 10; i += 2) f2[i] = 2u * f.v[i];
+  for (int i = 1; i < 10; i += 2) f2[i] = twice(f.v[i]);
   uint64_t carry = 0;
   uint32_t out[10];
 #pragma unroll
@@ -273,11 +287,11 @@ PV_HD void fe_sq(fe& h, const fe& f) {
   PV_CHECK_SQ(f);
   uint32_t f2[10], f19[10], f4[10];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) f2[i] = 2u * f.v[i];
+  for (int i = 0; i < 10; ++i) f2[i] = twice(f.v[i]);
 #pragma unroll
   for (int i = 5; i < 10; ++i) f19[i] = 19u * f.v[i];
 #pragma unroll
-  for (int i = 1; i < 10; i += 2) f4[i] = 4u * f.v[i];
+  for (int i = 1; i < 10; i += 2) f4[i] = twice(f2[i]);
   uint64_t carry = 0;
   uint32_t out[10];
 #pragma unroll
@@ -333,7 +347,7 @@ PV_HD void fe_mul_n(fe* const h[C], const fe* const f[C], const fe* const g[C]) 
 #pragma unroll
     for (int j = 1; j < 10; ++j) g19[c][j] = 19u * g[c]->v[j];
 #pragma unroll
-    for (int i = 1; i < 10; i += 2) f2[c][i] = 2u * f[c]->v[i];
+    for (int i = 1; i < 10; i += 2) f2[c][i] = twice(f[c]->v[i]);
   }
   uint64_t carry[C];
   uint32_t out[C][10];
@@ -381,11 +395,11 @@ PV_HD void fe_sq_n(fe* const h[C], const fe* const f[C]) {
   for (int c = 0; c < C; ++c) {
     PV_COUNT(sq);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) f2[c][i] = 2u * f[c]->v[i];
+    for (int i = 0; i < 10; ++i) f2[c][i] = twice(f[c]->v[i]);
 #pragma unroll
     for (int i = 5; i < 10; ++i) f19[c][i] = 19u * f[c]->v[i];
 #pragma unroll
-    for (int i = 1; i < 10; i += 2) f4[c][i] = 4u * f[c]->v[i];
+    for (int i = 1; i < 10; i += 2) f4[c][i] = twice(f2[c][i]);
   }
   uint64_t carry[C];
   uint32_t out[C][10];

@@ -129,6 +129,57 @@ void run(const char* name, const uint32_t* in, uint32_t* out, int cus, const uin
          "\"mad_per_s\": %.4e}\n", name, ok ? "true" : "false", dps, dps * 520.0);
 }
 
+// two independent squaring chains (the two pow22523 of decompressing -A and
+// -R): one after the other (production) vs interleaved with fe_sq2
+template <int V>
+__global__ __launch_bounds__(256, 2) void k_sqc(const uint32_t* in, uint32_t* out, int iters) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  fe x, y;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    x.v[i] = in[(t % 4096) * 30 + i];
+    y.v[i] = in[(t % 4096) * 30 + 10 + i];
+  }
+  if constexpr (V == 0) {
+#pragma unroll 1
+    for (int k = 0; k < iters; ++k) fe_sq(x, x);
+#pragma unroll 1
+    for (int k = 0; k < iters; ++k) fe_sq(y, y);
+  } else {
+#pragma unroll 1
+    for (int k = 0; k < iters; ++k) fe_sq2(x, x, y, y);
+  }
+  uint32_t w[8];
+  fe_add(x, x, y);
+  fe_tobytes_w(w, x);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[t * 8 + i] = w[i];
+}
+
+template <int V>
+void run_sq(const char* name, const uint32_t* in, uint32_t* out, int cus, const uint32_t* ref, uint32_t* host) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int blocks = cus * 2, iters = 1024;
+  float best = 1e30f;
+  for (int r = 0; r < 4; ++r) {
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(k_sqc<V>, dim3(blocks), dim3(256), 0, 0, in, out, iters);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    best = ms < best ? ms : best;
+  }
+  hipLaunchKernelGGL(k_sqc<V>, dim3(64), dim3(256), 0, 0, in, out, 37);
+  hipMemcpy(host, out, 64 * 256 * 8 * 4, hipMemcpyDeviceToHost);
+  const bool ok = memcmp(host, ref, 64 * 256 * 8 * 4) == 0;
+  const double sps = 2.0 * blocks * 256 * iters / (best * 1e-3);
+  printf("{\"test\": \"sq_chains\", \"variant\": \"%s\", \"waves_per_simd\": 2, \"ok\": %s, \"sq_per_s\": %.4e, "
+         "\"mad_per_s\": %.4e}\n", name, ok ? "true" : "false", sps, sps * 55.0);
+}
+
 int main() {
   int cus = 256;
   hipDeviceProp_t prop;
@@ -152,6 +203,12 @@ int main() {
   hipMemcpy(in, hin, nin * 4, hipMemcpyHostToDevice);
   uint32_t* ref = new uint32_t[64 * 256 * 8];
   uint32_t* host = new uint32_t[64 * 256 * 8];
+  hipLaunchKernelGGL(k_sqc<0>, dim3(64), dim3(256), 0, 0, in, out, 37);
+  hipMemcpy(ref, out, 64 * 256 * 8 * 4, hipMemcpyDeviceToHost);
+  for (int rep = 0; rep < 2; ++rep) {
+    run_sq<0>("serial", in, out, cus, ref, host);
+    run_sq<1>("sq2", in, out, cus, ref, host);
+  }
   hipLaunchKernelGGL(k_dbl<0>, dim3(64), dim3(256), 0, 0, in, out, 37);
   hipMemcpy(ref, out, 64 * 256 * 8 * 4, hipMemcpyDeviceToHost);
   for (int rep = 0; rep < 2; ++rep) {
