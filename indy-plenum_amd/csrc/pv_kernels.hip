@@ -57,8 +57,61 @@ __device__ __forceinline__ uint64_t take_index(unsigned long long* counter) {
   return (uint64_t)base + rank;
 }
 
+// Wave-private chunks of the global message queue: the wave takes CH indices
+// with one atomic and hands them out to its lanes by ballot rank; the atomic
+// for the NEXT chunk is issued when a chunk is opened and its result is only
+// read (v_readlane of lane 0) when that chunk is exhausted, so no lane ever
+// waits for an atomic round trip (k_hash refilled on nearly every trip on C4
+// and waited for take_index's atomic each time).  Must be called with the
+// whole wavefront active (convergent code).
+#ifndef PV_HASH_CHUNK
+#define PV_HASH_CHUNK 64
+#endif
+struct WaveQueue {
+  uint64_t cb;    // current chunk base
+  uint32_t cu;    // indices of the current chunk already handed out
+  uint64_t nbv;   // lane 0: base of the next chunk (atomic in flight)
+};
+
+__device__ __forceinline__ void wq_init(WaveQueue& q, unsigned long long* counter) {
+  const int lane = (int)(threadIdx.x & 63u);
+  unsigned long long b = 0, nb = 0;
+  if (lane == 0) {
+    b = atomicAdd(counter, (unsigned long long)PV_HASH_CHUNK);
+    nb = atomicAdd(counter, (unsigned long long)PV_HASH_CHUNK);
+  }
+  q.cb = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)b);
+  q.cu = 0;
+  q.nbv = nb;
+}
+
+// index for every lane with `want` (others get an unused value)
+__device__ __forceinline__ uint64_t wq_take(WaveQueue& q, bool want, unsigned long long* counter) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint64_t m = __ballot(want);
+  const uint32_t cnt = (uint32_t)__popcll(m);
+  const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  if (q.cu + cnt <= (uint32_t)PV_HASH_CHUNK) {
+    const uint64_t idx = q.cb + q.cu + rank;
+    q.cu += cnt;
+    return idx;
+  }
+  const uint32_t first = (uint32_t)PV_HASH_CHUNK - q.cu;
+  const uint64_t nb = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(q.nbv >> 32), 0) << 32) |
+                      __builtin_amdgcn_readlane((uint32_t)q.nbv, 0);
+  const uint64_t idx = rank < first ? q.cb + q.cu + rank : nb + (rank - first);
+  q.cb = nb;
+  q.cu = cnt - first;
+  if (lane == 0) q.nbv = atomicAdd(counter, (unsigned long long)PV_HASH_CHUNK);
+  return idx;
+}
+
 #ifndef PV_HASH_WAVES
 #define PV_HASH_WAVES 2
+#endif
+#ifndef PV_HASH_LDS
+#define PV_HASH_LDS 0
 #endif
 // libsodium's pre-checks on (R, S, A), one
 // lane per signature, ahead of the hash: keeps the branchy, load-dependent
@@ -87,7 +140,9 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
   uint64_t hs[8];
   uint32_t ra[16];   // R || A of the current message (block 0's prefix)
   // prefetched next message: offsets, pre-check verdict, R || A
-  uint64_t nidx = take_index(counter), nmo = 0, nme = 0;
+  WaveQueue q;
+  wq_init(q, counter);
+  uint64_t nidx = wq_take(q, true, counter), nmo = 0, nme = 0;
   uint32_t nok = 0, nra[16];
   auto prefetch = [&]() {
     if (nidx < n) {
@@ -99,37 +154,106 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
     }
   };
   prefetch();
+#if PV_HASH_LDS
+  // Message blocks are staged through LDS by the whole wavefront: lane l's
+  // 144-byte window (9 groups of 16 B) is cut into 9 parts and part p is
+  // loaded by lane (9 l + p) % 64 in pass (9 l + p) / 64, so one load
+  // instruction of the wave covers ~7 consecutive windows (2 cache lines each)
+  // instead of 64 scattered ones (~4.5x fewer L1 tag lookups per block).
+  // Measured slower than per-lane loads (profiles/r02_ab_hash_queue.json):
+  // the kernel is not bound by the L1 tag rate.
+  constexpr int WB = 144;   // window bytes per lane
+  __shared__ uint4 win[HASH_BLOCK / 64][64 * WB / 16];
+  __shared__ uint4 desc[HASH_BLOCK / 64][64];
+  const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
+#endif
+  // Convergent loop: every lane runs every trip (queue takes are wave-wide);
+  // a lane without a block in progress idles through the compression.
   while (true) {
-    // refill from the prefetched message, then prefetch the one after it
-    while (blk == nblk && nidx < n) {
+    // a lane whose message is done promotes its prefetched next message (a
+    // message that failed the pre-checks leaves it idle for one trip) and
+    // takes a new next index
+    const bool promote = blk == nblk && nidx < n;
+    if (promote) {
       idx = nidx;
-      const bool ok = nok != 0;
       mo = nmo;
       ml = nme - nmo;
 #pragma unroll
       for (int j = 0; j < 16; ++j) ra[j] = nra[j];
-      nidx = take_index(counter);
-      prefetch();
-      if (ok) {
+      if (nok != 0) {
         nblk = hram_blocks(ml);
         blk = 0;
         sha512_init(hs);
       }
     }
-    if (blk == nblk) break;   // queue drained and no message in progress
+    const uint64_t t = wq_take(q, promote, counter);
+    if (promote) {
+      nidx = t;
+      prefetch();
+    }
+    const bool active = blk < nblk;
+    if (!__any(active || nidx < n)) break;   // nothing in progress, nothing queued
     uint64_t w[16];
+#if PV_HASH_LDS
     {
+      // this lane's window: aligned-down start of block blk and the number of
+      // 16-byte groups holding message bytes (msg_fetch's rule)
+      const uint64_t qb = hram_q(blk);
+      const uint8_t* m = blob + mo;
+      const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + qb) & 3u);
+      const int64_t rem = (int64_t)ml - (int64_t)qb;
+      int ng = 0;
+      if (active && rem + (int64_t)mis > 0) {
+        const int64_t g = (rem + (int64_t)mis + 15) / 16;
+        ng = (int)(g < (blk == 0 ? 5 : 9) ? g : (blk == 0 ? 5 : 9));
+      }
+      const uint64_t wa = reinterpret_cast<uint64_t>(m + qb - mis);
+      desc[wv][lane] = make_uint4((uint32_t)wa, (uint32_t)(wa >> 32), (uint32_t)ng, 0u);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int gi = 64 * k + lane, owner = gi / 9, part = gi - 9 * (gi / 9);
+        const uint4 d = desc[wv][owner];
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (part < (int)d.z) {
+          const uint64_t a = ((uint64_t)d.y << 32 | d.x) + 16u * (uint32_t)part;
+          const uint32_t* p = reinterpret_cast<const uint32_t*>(a);
+          v = make_uint4(p[0], p[1], p[2], p[3]);
+        }
+        win[wv][gi] = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint32_t y[MSG_Y];
+#pragma unroll
+      for (int g = 0; g < 9; ++g) {
+        const uint4 v = win[wv][9 * lane + g];
+        y[4 * g] = v.x;
+        y[4 * g + 1] = v.y;
+        y[4 * g + 2] = v.z;
+        y[4 * g + 3] = v.w;
+      }
+      __builtin_amdgcn_wave_barrier();   // the next trip's stores come after these reads
+      if (active) hram_assemble_ra(w, y, ra, m, ml, blk, nblk);
+    }
+#endif
+    if (active) {
+#if !PV_HASH_LDS
       uint32_t y[MSG_Y];
       msg_fetch(y, blob + mo, ml, hram_q(blk), blk == 0);
       hram_assemble_ra(w, y, ra, blob + mo, ml, blk, nblk);
-    }
-    sha512_compress(hs, w);
-    if (++blk == nblk) {
-      uint32_t d[16];
-      sha512_digest_words(d, hs);
-      uint32_t* o = dig + 16 * idx;
+#endif
+      sha512_compress(hs, w);
+      if (++blk == nblk) {
+        uint32_t d[16];
+        sha512_digest_words(d, hs);
+        uint32_t* o = dig + 16 * idx;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) o[k] = d[k];
+        for (int k = 0; k < 16; ++k) o[k] = d[k];
+      }
     }
   }
 }
@@ -559,30 +683,49 @@ hipError_t launch_tally_bits(const uint32_t* bits, const uint32_t* dup, uint64_t
 
 // ----------------------------------------------- SHA-256 / Merkle (row f3)
 // Batch SHA-256 of (prefix || M_i): persistent lanes with per-lane refill, the
-// same work-queue scheme as k_hash (ragged messages cost no divergence).
+// same work-queue scheme as k_hash (ragged messages cost no divergence;
+// wave-private index chunks, next message's offsets loaded one message ahead).
 __global__ __launch_bounds__(256) void k_sha256(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
                                                  uint64_t n, uint32_t plen, uint32_t prefix,
                                                  unsigned long long* __restrict__ counter, uint32_t* __restrict__ out) {
-  uint64_t idx = take_index(counter);
-  uint64_t blk = 0, nblk = 0, mo = 0, ml = 0;
+  WaveQueue q;
+  wq_init(q, counter);
+  uint64_t idx = n, blk = 0, nblk = 0, mo = 0, ml = 0;
+  uint64_t nidx = wq_take(q, true, counter), nmo = 0, nme = 0;
+  if (nidx < n) {
+    nmo = off[nidx];
+    nme = off[nidx + 1];
+  }
   uint32_t hs[8];
   while (true) {
-    if (blk == nblk && idx < n) {
-      mo = off[idx];
-      ml = off[idx + 1] - mo;
+    const bool promote = blk == nblk && nidx < n;
+    if (promote) {
+      idx = nidx;
+      mo = nmo;
+      ml = nme - nmo;
       nblk = sha256_blocks(ml, plen);
       blk = 0;
       sha256_init(hs);
     }
-    if (idx >= n) break;
-    uint32_t w[16];
-    sha256_block(w, blob + mo, ml, plen, prefix, blk, nblk);
-    sha256_compress(hs, w);
-    if (++blk == nblk) {
-      uint32_t* o = out + 8 * idx;
+    const uint64_t t = wq_take(q, promote, counter);
+    if (promote) {
+      nidx = t;
+      if (nidx < n) {
+        nmo = off[nidx];
+        nme = off[nidx + 1];
+      }
+    }
+    const bool active = blk < nblk;
+    if (!__any(active)) break;   // every message promotes on the trip it is taken
+    if (active) {
+      uint32_t w[16];
+      sha256_block(w, blob + mo, ml, plen, prefix, blk, nblk);
+      sha256_compress(hs, w);
+      if (++blk == nblk) {
+        uint32_t* o = out + 8 * idx;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = bswap32_(hs[k]);
-      idx = take_index(counter);
+        for (int k = 0; k < 8; ++k) o[k] = bswap32_(hs[k]);
+      }
     }
   }
 }
