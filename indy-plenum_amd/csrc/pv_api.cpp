@@ -565,7 +565,7 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     d.last_ws = (int)(&w - d.ws);
   } else {
     HIP_OK(pv::launch_curve(pk, sig, w.h.p, w.pre.p, d.btab.p, w.scratch.p, w.scratch.cap / pv::ATAB_WORDS, verdict,
-                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p));
+                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p, w.qc.p + 1));
   }
   if (lev) HIP_OK(hipEventRecord(lev[2], s));
   if (timed) {

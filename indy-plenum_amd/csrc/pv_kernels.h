@@ -46,7 +46,8 @@ hipError_t launch_hash(const uint8_t* pk, const uint8_t* sig, const uint8_t* blo
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab = nullptr,
-                        const uint32_t* kidx = nullptr, const uint32_t* bw = nullptr);
+                        const uint32_t* kidx = nullptr, const uint32_t* bw = nullptr,
+                        unsigned long long* tasks = nullptr);   // wave task queue counter (zeroed here)
 
 // Half-size scalar path (generic batches, pv_lattice.h):
 //   launch_lattice   pre-checks (-> pre) and h mod L -> (c, d, s') records

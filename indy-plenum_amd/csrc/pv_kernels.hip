@@ -107,6 +107,19 @@ __device__ __forceinline__ uint64_t wq_take(WaveQueue& q, bool want, unsigned lo
   return idx;
 }
 
+// Next wave task from a global counter, as a wave-UNIFORM value: every lane
+// takes part in the atomic (lane 0 adds 1, the others 0, so lane 0's return is
+// the task) and the result is read with v_readfirstlane, so a loop exit on it
+// is a uniform branch.  (An `if (lane == 0) atomicAdd` + __shfl made the
+// compiler treat the exit as divergent; with the grouped k_curve it then
+// structurized the loop so that the shuffle re-read a stale value and the
+// wave never left it.)  Call with the whole wavefront active.
+__device__ __forceinline__ uint64_t wave_task(unsigned long long* tasks) {
+  const unsigned long long v = atomicAdd(tasks, (threadIdx.x & 63u) == 0 ? 1ull : 0ull);
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 #ifndef PV_HASH_WAVES
 #define PV_HASH_WAVES 2
 #endif
@@ -310,7 +323,8 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
                                                                         uint64_t* __restrict__ bitmap, uint64_t n,
                                                                         const uint32_t* __restrict__ ktab,
                                                                         const uint32_t* __restrict__ kidx,
-                                                                        const uint32_t* __restrict__ bw) {
+                                                                        const uint32_t* __restrict__ bw,
+                                                                        unsigned long long* __restrict__ tasks) {
   // generic kernel: radix-256 table q = 0 in LDS (16.5 KB); the comb kernel of
   // prepared keys reads the radix-2^16 chunk tables bw from L2/MALL
   constexpr int TW = BTAB_ENTRIES * BTAB_WORDS;
@@ -319,19 +333,29 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
     for (int j = threadIdx.x; j < TW; j += CURVE_BLOCK) btab[j] = btab_g[j];
     __syncthreads();
   }
-  const uint64_t nthreads = (uint64_t)gridDim.x * CURVE_BLOCK;
+  // persistent waves over a queue of wave tasks: task t = signatures
+  // [64 CURVE_K t, 64 CURVE_K (t + 1)), lane l holding t's signatures l, l + 64,
+  // ... (coalesced per k).  A dynamic queue (one atomic per task) instead of a
+  // static grid stride: the grid's tail is one task per wave, and a block that
+  // starts late (its CU busy with another stream's kernel) delays nothing.
+  const int ln = (int)(threadIdx.x & 63u);
   const uint64_t gid = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
   uint32_t* lane = scratch + gid * LANE_WORDS;
-  for (uint64_t base = 0; base < n; base += CURVE_K * nthreads) {
-    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, base + gid, nthreads, n, lane, btab, ktab, kidx, bw);
+  constexpr uint64_t PER = 64ull * CURVE_K;
+  const uint64_t ntasks = (n + PER - 1) / PER;
+  for (;;) {
+    const uint64_t t = wave_task(tasks);
+    if (t >= ntasks) break;
+    const uint64_t i0 = t * PER + (uint64_t)ln;
+    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, i0, 64, n, lane, btab, ktab, kidx, bw);
 #pragma unroll
     for (int k = 0; k < CURVE_K; ++k) {
-      const uint64_t i = base + (uint64_t)k * nthreads + gid;
+      const uint64_t i = i0 + 64ull * (uint64_t)k;
       const bool ok = (okm >> k) & 1u;
       const uint64_t ball = __ballot(ok);
       if (i < n) {
         verdict[i] = ok ? 1 : 0;
-        if ((threadIdx.x & 63) == 0) bitmap[i >> 6] = ball;
+        if (ln == 0) bitmap[i >> 6] = ball;
       }
     }
   }
@@ -349,19 +373,24 @@ hipError_t curve_occupancy(int* blocks_per_cu, bool keyed) {
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab,
-                        const uint32_t* kidx, const uint32_t* bw) {
+                        const uint32_t* kidx, const uint32_t* bw, unsigned long long* tasks) {
   if (n == 0) return hipSuccess;
-  uint64_t need = (n + (uint64_t)CURVE_BLOCK * CURVE_K - 1) / ((uint64_t)CURVE_BLOCK * CURVE_K);
+  // one wave task = 64 * CURVE_K signatures, CURVE_BLOCK / 64 waves per block
+  const uint64_t ntasks = (n + 64ull * CURVE_K - 1) / (64ull * CURVE_K);
+  uint64_t need = (ntasks + CURVE_BLOCK / 64 - 1) / (CURVE_BLOCK / 64);
   uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
   if (b * CURVE_BLOCK > scratch_lanes) b = scratch_lanes / CURVE_BLOCK;
   if (b == 0) return hipErrorInvalidValue;
   if (ktab && !bw) return hipErrorInvalidValue;
+  if (!tasks) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(tasks, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
   if (ktab)
     hipLaunchKernelGGL(k_curve<true>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
-                       verdict, bitmap, n, ktab, kidx, bw);
+                       verdict, bitmap, n, ktab, kidx, bw, tasks);
   else
     hipLaunchKernelGGL(k_curve<false>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
-                       verdict, bitmap, n, nullptr, nullptr, nullptr);
+                       verdict, bitmap, n, nullptr, nullptr, nullptr, tasks);
   return hipGetLastError();
 }
 
@@ -422,9 +451,7 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve_half(
   const uint64_t full_tasks = (nd + 63) / 64;
   const uint64_t all_tasks = full_tasks + (n + 63) / 64;
   for (;;) {
-    unsigned long long t = 0;
-    if (lane == 0) t = atomicAdd(tasks, 1ull);
-    t = __shfl(t, 0, 64);
+    const uint64_t t = wave_task(tasks);
     if (t >= all_tasks) break;
     if (t < full_tasks) {
       const uint64_t j = t * 64 + lane;
