@@ -275,9 +275,10 @@ struct KeyIndex {
 enum class CurveMode { Half, Full, Grouped };
 
 // Verify workspaces and the compute stream they are used on.  Device-pointer
-// calls use ws[0] (stream = the device stream or the caller's); the host-buffer
-// pipeline alternates chunks over ws[0] and ws[1] on two compute streams, so
-// the kernels of chunk c + 1 fill the tail of chunk c's persistent grid
+// calls use ws[0] (stream = the device stream or the caller's; pv_*_async:
+// ws[slot]); the host-buffer pipeline alternates chunks over ws[0] and ws[1]
+// on their two streams, so the kernels of chunk c + 1 fill the tail of chunk
+// c's persistent grid
 // instead of waiting for it (the scratch of concurrently running curve grids
 // must not alias: one per workspace).
 struct Workspace {
@@ -454,12 +455,12 @@ int init_device(Device& d) {
 void release_device(Device& d) {
   if (d.id < 0) return;
   (void)hipSetDevice(d.id);
-  if (d.stream) (void)hipStreamSynchronize(d.stream);
-  if (d.ws[1].stream) (void)hipStreamSynchronize(d.ws[1].stream);
+  for (auto& w : d.ws)
+    if (w.stream) (void)hipStreamSynchronize(w.stream);
   d.btab.release(); d.bw.release(); d.counter.release();
   for (auto& w : d.ws) w.release();
   if (d.ws[1].stream) (void)hipStreamDestroy(d.ws[1].stream);
-  d.ws[1].stream = d.ws[0].stream = nullptr;
+  for (auto& w : d.ws) w.stream = nullptr;
   d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
   d.off.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release(); d.tflag.release(); d.tbits.release();
@@ -503,6 +504,66 @@ int resolve_live(Device& d) {
   return PV_OK;
 }
 
+// The two stages of a verify for device-resident inputs, on stream s with
+// workspace w.  prep: pre-checks + SHA-512 (+ the lattice stage of the
+// half-size path); curve: the curve kernel writing verdicts + bitmap.
+// `bm` = the caller's bitmap or null (then w.bitmap).
+uint64_t* stage_bitmap(Workspace& w, uint64_t* bitmap, uint64_t n, int& rc) {
+  rc = PV_OK;
+  if (bitmap) return bitmap;
+  const hipError_t e = w.bitmap.ensure((n + 63) / 64);
+  if (e != hipSuccess)
+    rc = fail(e == hipErrorOutOfMemory ? PV_ENOMEM : PV_EIO, "bitmap allocation failed: %s", hipGetErrorString(e));
+  return w.bitmap.p;
+}
+
+int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
+                 const uint64_t* off, uint64_t n, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
+                 const uint32_t* kidx) {
+  HIP_OK(w.h.ensure(n * 16));
+  HIP_OK(w.pre.ensure(n));
+  HIP_OK(w.counter.ensure(1));
+  HIP_OK(w.qc.ensure(2));
+  HIP_OK(w.scratch.ensure(d.scratch_words));
+  const bool half = !ktab && d.mode != CurveMode::Grouped;
+  if (half) {
+    if (n > 0xffffffffull) return fail(PV_EINVAL, "at most 2^32-1 signatures per device call");
+    HIP_OK(w.hrec.ensure(n * pv::HSREC_WORDS));
+    HIP_OK(w.dlist.ensure(n));
+  }
+  // the half-size path runs the pre-checks in k_lattice (k_hash hashes every
+  // signature); keyed and grouped batches in k_precheck before the hash
+  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, w.counter.p, w.h.p, half ? nullptr : w.pre.p, d.hash_blocks, s, kidx));
+  if (half)
+    HIP_OK(pv::launch_lattice(pk, sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
+                              d.mode == CurveMode::Full, s));
+  return PV_OK;
+}
+
+int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, uint64_t n, uint8_t* verdict,
+                  uint64_t* bm, hipStream_t s, const uint32_t* ktab, const uint32_t* kidx) {
+  const bool half = !ktab && d.mode != CurveMode::Grouped;
+  if (half && n <= d.lat_max) {
+    // small batch: lane pairs per signature (shorter per-lane chain), one
+    // table of scratch per lane
+    HIP_OK(w.scratch.ensure(std::max<size_t>(d.scratch_words, (size_t)((2 * n + 63) / 64 * 64) * pv::ATAB_LAT_WORDS)));
+    HIP_OK(pv::launch_curve_lat(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
+                                w.scratch.cap / pv::ATAB_LAT_WORDS, verdict, bm, n, s));
+    w.half_ran = true;
+    d.last_ws = (int)(&w - d.ws);
+  } else if (half) {
+    HIP_OK(pv::launch_curve_half(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
+                                 w.scratch.cap / pv::HALF_SCRATCH_WORDS, verdict, bm, n, w.dlist.p, w.qc.p, w.qc.p + 1,
+                                 d.curve_half_blocks, s));
+    w.half_ran = true;
+    d.last_ws = (int)(&w - d.ws);
+  } else {
+    HIP_OK(pv::launch_curve(pk, sig, w.h.p, w.pre.p, d.btab.p, w.scratch.p, w.scratch.cap / pv::ATAB_WORDS, verdict,
+                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p, w.qc.p + 1));
+  }
+  return PV_OK;
+}
+
 // enqueue hash + curve for device-resident inputs on stream s with workspace w
 int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                    const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed,
@@ -522,51 +583,18 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     lev = d.live_pool[d.live_used++].e;
     ++d.live_launches;
   }
-  HIP_OK(w.h.ensure(n * 16));
-  HIP_OK(w.pre.ensure(n));
-  HIP_OK(w.counter.ensure(1));
-  HIP_OK(w.qc.ensure(2));
-  HIP_OK(w.scratch.ensure(d.scratch_words));
-  uint64_t* bm = bitmap;
-  if (!bm) {
-    HIP_OK(w.bitmap.ensure((n + 63) / 64));
-    bm = w.bitmap.p;
-  }
-  const bool half = !ktab && d.mode != CurveMode::Grouped;
-  if (half) {
-    if (n > 0xffffffffull) return fail(PV_EINVAL, "at most 2^32-1 signatures per device call");
-    HIP_OK(w.hrec.ensure(n * pv::HSREC_WORDS));
-    HIP_OK(w.dlist.ensure(n));
-  }
+  int rc = PV_OK;
+  uint64_t* bm = stage_bitmap(w, bitmap, n, rc);
+  if (rc) return rc;
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
   if (lev) HIP_OK(hipEventRecord(lev[0], s));
-  // the half-size path runs the pre-checks in k_lattice (k_hash hashes every
-  // signature); keyed and grouped batches in k_precheck before the hash
-  HIP_OK(pv::launch_hash(pk, sig, blob, off, n, w.counter.p, w.h.p, half ? nullptr : w.pre.p, d.hash_blocks, s, kidx));
+  rc = enqueue_prep(d, w, pk, sig, blob, off, n, bm, s, ktab, kidx);
+  if (rc) return rc;
   // the "hash" interval also holds the scalar stage of the half-size path
-  if (half)
-    HIP_OK(pv::launch_lattice(pk, sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
-                              d.mode == CurveMode::Full, s));
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (lev) HIP_OK(hipEventRecord(lev[1], s));
-  if (half && n <= d.lat_max) {
-    // small batch: lane pairs per signature (shorter per-lane chain), one
-    // table of scratch per lane
-    HIP_OK(w.scratch.ensure(std::max<size_t>(d.scratch_words, (size_t)((2 * n + 63) / 64 * 64) * pv::ATAB_LAT_WORDS)));
-    HIP_OK(pv::launch_curve_lat(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
-                                w.scratch.cap / pv::ATAB_LAT_WORDS, verdict, bm, n, s));
-    w.half_ran = true;
-    d.last_ws = (int)(&w - d.ws);
-  } else if (half) {
-    HIP_OK(pv::launch_curve_half(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
-                                 w.scratch.cap / pv::HALF_SCRATCH_WORDS, verdict, bm, n, w.dlist.p, w.qc.p, w.qc.p + 1,
-                                 d.curve_half_blocks, s));
-    w.half_ran = true;
-    d.last_ws = (int)(&w - d.ws);
-  } else {
-    HIP_OK(pv::launch_curve(pk, sig, w.h.p, w.pre.p, d.btab.p, w.scratch.p, w.scratch.cap / pv::ATAB_WORDS, verdict,
-                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p, w.qc.p + 1));
-  }
+  rc = enqueue_curve(d, w, pk, sig, n, verdict, bm, s, ktab, kidx);
+  if (rc) return rc;
   if (lev) HIP_OK(hipEventRecord(lev[2], s));
   if (timed) {
     HIP_OK(hipEventRecord(d.ev[2], s));
@@ -593,11 +621,9 @@ struct HostBatch {
 // calling thread: key dedup and buffers, then a pipeline of chunks.  Chunk c's
 // inputs are gathered by host threads into page-locked slot c & 1 (its
 // offsets rebased to the shard and checked while they are copied), DMA'd on
-// the copy stream, and verified on compute stream c & 1 with workspace c & 1:
-// chunk c + 1's kernels start while chunk c's curve grid drains, so chunked
-// launches pay no tail.  Verdicts come back through a page-locked buffer.
-// Returns after every verdict of the shard is in hb.verdict (or on error,
-// after the device has drained).
+// the copy stream, and verified on workspace c & 1's stream (see the loop).
+// Verdicts come back through a page-locked buffer.  Returns after every verdict of the
+// shard is in hb.verdict (or on error, after the device has drained).
 int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   const uint64_t m = e - s;
   if (m == 0) return PV_OK;
@@ -713,6 +739,11 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   auto us = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tstart).count(); };
   if (trace) fprintf(stderr, "[pv host] dev %d shard %llu sigs: setup %.1f us, %zu chunks, pinned %d\n", d.id,
                      (unsigned long long)m, us(), nch, (int)pinned);
+  // chunk c is verified on workspace c & 1 and its stream, so chunk c + 1's
+  // kernels start while chunk c's curve grid drains.  (A separate prep stream
+  // for every chunk's hash + lattice with three workspaces measured no better:
+  // squeezed into the slots the curve grids leave, the prep kernels of a chunk
+  // take ~1.1 ms either way -- profiles/r02_e2e_timeline_prepstream_notadopted.txt.)
   for (size_t c = 0; c < nch; ++c) {
     const uint64_t c0 = bounds[c], c1 = bounds[c + 1], mc = c1 - c0;
     Workspace& w = d.ws[c & 1];
@@ -1033,7 +1064,7 @@ int pv_set_curve_mode(uint32_t mode) {
   if (mode > PV_CURVE_GROUPED) return fail(PV_EINVAL, "unknown curve mode %u", mode);
   for (auto& d : g_devs) {
     d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
-    d.ws[0].half_ran = d.ws[1].half_ran = false;
+    for (auto& w : d.ws) w.half_ran = false;
   }
   return PV_OK;
 }
