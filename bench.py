@@ -530,12 +530,23 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    calib = 0
+    if pipelined:
+        # the kernels' own durations: a few steps one after the other with HIP
+        # events on the launch stream, right before the timed region (pipelined
+        # launches overlap, so their intervals hold the other stream's work)
+        calib = 5
+        nat.kernel_timing(local, True)
+        for _ in range(calib):
+            batch.verify()
+        torch.cuda.synchronize()
+        calib_sums = nat.kernel_timing(local, False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     # HIP events around each verify launch of the timed steps (sequential
     # schedule); pipelined launches overlap, so their kernels are timed on
-    # sequential calibration steps after the timed region instead
+    # the sequential calibration steps before the timed region instead
     nat.kernel_timing(local, not pipelined)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -590,18 +601,10 @@ def main():
     # kernel-level timing for the roofline: HIP events on the launch stream,
     # recorded during the timed steps above (averaged over those launches)
     h_sum, c_sum, launches = nat.kernel_timing(local, False)
-    calib = 0
     if pipelined:
-        # kernel durations on their own: a few steps, one after the other, with
-        # HIP events on the launch stream (outside the timed region)
-        calib = 3
-        nat.kernel_timing(local, True)
-        for _ in range(calib):
-            batch.verify()
-        torch.cuda.synchronize()
-        h_sum, c_sum, launches = nat.kernel_timing(local, False)
+        h_sum, c_sum, launches = calib_sums
     ms_hash, ms_curve = h_sum / max(1, launches), c_sum / max(1, launches)
-    kernel_ms_on = ('{} sequential calibration steps right after the timed region (pipelined launches overlap)'
+    kernel_ms_on = ('{} sequential calibration steps right before the timed region (pipelined launches overlap)'
                     .format(calib) if pipelined else 'the timed steps')
     curve_mode, deferred = nat.curve_stats(local)
     if key_cache:
@@ -620,7 +623,7 @@ def main():
     # the dominant kernel is priced on its own HIP-event duration: in the timed
     # steps when they run one after the other; when they are pipelined the
     # launches overlap (a launch's interval includes the other stream's tail),
-    # so on the sequential calibration steps right after the timed region.
+    # so on the sequential calibration steps right before the timed region.
     # per_step: the same work over the pipelined per-step time, every kernel of
     # the step charged to the curve (a lower bound on its rate).
     achieved = work / (ms_curve * 1e-3)

@@ -23,25 +23,48 @@ struct ge_niels { fe ypx, ymx, xy2d; };
 
 PV_HD void ge_p3_0(ge_p3& h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); fe_0(h.T); }
 
-// Independent products go through the fused forms (fe_mul2 / fe_sq2: two
-// column chains interleaved, pv_field.h): +8 % doublings/s on gfx950 at the
-// curve kernel's 2 waves/SIMD (tools/ubench/fe_ilp.hip); pairs beat triples.
+// PV_FUSE selects where independent products go through the fused forms
+// (fe_mul2 / fe_sq2: two column chains interleaved in one asm block,
+// pv_field.h): bit 0 the doubling's squarings, bit 1 the p1p1 conversions,
+// bit 2 the table-entry additions (pv_verify_core.h).  Same values either way.
+#ifndef PV_FUSE
+#define PV_FUSE 0
+#endif
 PV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+#if PV_FUSE & 2
   fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+#else
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+#endif
   fe_mul(r.Z, p.Z, p.T);
 }
 
 PV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+#if PV_FUSE & 2
   fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fe_mul2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
+#else
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+#endif
 }
 
 // dbl-2008-hwcd (a = -1) from p2:  r.X = 2XY, r.Y = Y^2+X^2, r.Z = Y^2-X^2, r.T = 2Z^2-(Y^2-X^2)
 PV_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe xx, yy, zz2, xy2, t;
   fe_add(t, p.X, p.Y);         // LOOSE
+#if PV_FUSE & 1
   fe_sq2(xx, p.X, yy, p.Y);
   fe_sq2(zz2, p.Z, xy2, t);    // Z^2, (X+Y)^2
+#else
+  fe_sq(xx, p.X);
+  fe_sq(yy, p.Y);
+  fe_sq(zz2, p.Z);
+  fe_sq(xy2, t);               // (X+Y)^2
+#endif
   fe_add(r.Y, yy, xx);         // LOOSE
   fe_sub(r.Z, yy, xx);         // LOOSE
   fe_sub4(r.X, xy2, r.Y);      // (X+Y)^2 - X^2 - Y^2 = 2XY, even limbs < 2^28.4:

@@ -404,10 +404,24 @@ PV_HD void load_entry(ge_entry& e, const uint32_t* q, bool neg) {
 // same operation sequence (and operand bounds) as ge_add_cached_at
 PV_HD void ge_add_entry(ge_p1p1& r, const ge_p3& p, const ge_entry& e, bool neg) {
   fe c, d, a, b, u, v;
+#if PV_FUSE & 4
   fe_mul2(c, e.t2d, p.T, d, p.Z, e.z2);
   fe_add(u, p.Y, p.X);
   fe_sub(v, p.Y, p.X);
+#if PV_FUSE & 4
   fe_mul2(a, u, e.a, b, v, e.b);
+#else
+  fe_mul(a, u, e.a);
+  fe_mul(b, v, e.b);
+#endif
+#else
+  fe_mul(c, e.t2d, p.T);
+  fe_mul(d, p.Z, e.z2);
+  fe_add(u, p.Y, p.X);
+  fe_mul(a, u, e.a);
+  fe_sub(v, p.Y, p.X);
+  fe_mul(b, v, e.b);
+#endif
   fe_sub(r.X, a, b);
   fe_add(r.Y, a, b);
   fe_neg(u, c);
@@ -433,7 +447,12 @@ PV_HD void ge_madd_entry(ge_p1p1& r, const ge_p3& p, const ge_nentry& e, bool ne
   fe_carry(d);
   fe_add(u, p.Y, p.X);
   fe_sub(v, p.Y, p.X);
+#if PV_FUSE & 4
   fe_mul2(a, u, e.a, b, v, e.b);
+#else
+  fe_mul(a, u, e.a);
+  fe_mul(b, v, e.b);
+#endif
   fe_sub(r.X, a, b);
   fe_add(r.Y, a, b);
   fe_neg(u, c);
