@@ -100,7 +100,7 @@ def _mad_peak():
 
 def _traffic_per_launch():
     """HBM bytes per curve launch from the committed rocprofv3 PMC summary, or None."""
-    path = os.path.join(REPO, 'profiles', 'r01s5_curve_pmc.json')
+    path = os.path.join(REPO, 'profiles', 'r02_curve_pmc.json')
     try:
         with open(path) as fh:
             return json.load(fh).get('hbm_bytes_per_launch')
