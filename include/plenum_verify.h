@@ -261,13 +261,21 @@ int pv_set_curve_mode(uint32_t mode);
 
 /* Latency mode of the half-size path: generic batches of at most
  * max_signatures signatures (per device call / host-buffer chunk) run the
- * curve stage on lane PAIRS -- one lane holds A and the low half of s'B, the
- * other R and the high half; they add their points at the end -- so each
- * lane's sequential chain is ~30 % shorter (one decompression, one table, half
- * the adds): small batches, where a few waves occupy the GPU, finish sooner.
- * Larger batches keep the one-lane-per-signature throughput kernel.  Verdicts
- * are identical.  Default 2048, env PV_LAT_MAX at pv_init; 0 disables. */
+ * curve stage on 8 lanes per signature -- the lane-pair split (one side holds
+ * A and the low half of s'B, the other R and the high half; they add their
+ * points at the end), each side's point spread over a lane QUAD (one
+ * coordinate per lane, DPP exchanges), so a doubling costs each lane one
+ * squaring + one multiply: small batches, where a few waves occupy the GPU,
+ * finish ~2x sooner.  Deferred records run in the same kernel.  Larger
+ * batches keep the one-lane-per-signature throughput kernel.  Verdicts are
+ * identical.  Default 2048, env PV_LAT_MAX at pv_init; 0 disables. */
 int pv_set_lat_max(uint64_t max_signatures);
+/* Latency kernel: PV_LAT_QUAD (default, lane quads per point) or PV_LAT_PAIR
+ * (the previous lane-pair kernel, one lane per point; A/B).  Env
+ * PV_LAT_KERNEL=quad|pair at pv_init. */
+#define PV_LAT_QUAD 0u
+#define PV_LAT_PAIR 1u
+int pv_set_lat_kernel(uint32_t kernel);
 int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 
 /* Live kernel timing of the verify calls themselves (bench.py's timed region):

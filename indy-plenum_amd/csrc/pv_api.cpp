@@ -46,7 +46,7 @@ int fail(int code, const char* fmt, ...) {
 #define PV_HOST_CHUNKS 8
 #define PV_HOST_CHUNK_MIN 32768
 // generic batches of at most this many signatures run the latency-mode curve
-// kernel (lane pairs per signature); PV_LAT_MAX env overrides (0 disables)
+// kernel (k_curve_quad: lane quads per point); PV_LAT_MAX env overrides (0 disables)
 #define PV_LAT_MAX 2048
 // shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
 #define PV_DEDUP_SAMPLE_MIN 262144
@@ -309,7 +309,8 @@ struct Device {
   int copy_threads = PV_HOST_COPY_THREADS;
   int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
   size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
-  uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use k_curve_lat; PV_LAT_MAX env (0 = off)
+  uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; PV_LAT_MAX env (0 = off)
+  bool lat_quad = true;              // latency kernel: k_curve_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
   PinBuf pin[2];
   std::shared_ptr<GatherPool> pool = std::make_shared<GatherPool>();  // host gather threads
   PinBuf vout;  // page-locked verdicts of the shard (D2H target; copied to the caller after the drain)
@@ -392,6 +393,10 @@ int init_device(Device& d) {
     const long v = atol(t);
     if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_MAX must be in 0..1048576 (got %s)", t);
     d.lat_max = (uint64_t)v;
+  }
+  if (const char* m = getenv("PV_LAT_KERNEL")) {
+    if (!strcmp(m, "pair")) d.lat_quad = false;
+    else if (strcmp(m, "quad") != 0) return fail(PV_EINVAL, "PV_LAT_KERNEL must be quad or pair (got %s)", m);
   }
   if (const char* t = getenv("PV_HOST_PIN_MAX_MB")) {
     const long mb = atol(t);
@@ -543,9 +548,13 @@ int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig,
 int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, uint64_t n, uint8_t* verdict,
                   uint64_t* bm, hipStream_t s, const uint32_t* ktab, const uint32_t* kidx) {
   const bool half = !ktab && d.mode != CurveMode::Grouped;
-  if (half && n <= d.lat_max) {
-    // small batch: lane pairs per signature (shorter per-lane chain), one
-    // table of scratch per lane
+  if (half && n <= d.lat_max && d.lat_quad) {
+    // small batch: 8 lanes per signature, each point on a lane quad
+    HIP_OK(pv::launch_curve_quad(pk, sig, w.hrec.p, d.bw.p, verdict, bm, n, s));
+    w.half_ran = true;
+    d.last_ws = (int)(&w - d.ws);
+  } else if (half && n <= d.lat_max) {
+    // (PV_LAT_KERNEL=pair) lane pairs per signature, one table of scratch per lane
     HIP_OK(w.scratch.ensure(std::max<size_t>(d.scratch_words, (size_t)((2 * n + 63) / 64 * 64) * pv::ATAB_LAT_WORDS)));
     HIP_OK(pv::launch_curve_lat(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
                                 w.scratch.cap / pv::ATAB_LAT_WORDS, verdict, bm, n, s));
@@ -1066,6 +1075,14 @@ int pv_set_curve_mode(uint32_t mode) {
     d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
     for (auto& w : d.ws) w.half_ran = false;
   }
+  return PV_OK;
+}
+
+int pv_set_lat_kernel(uint32_t kernel) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (kernel > PV_LAT_PAIR) return fail(PV_EINVAL, "unknown latency kernel %u", kernel);
+  for (auto& d : g_devs) d.lat_quad = kernel == PV_LAT_QUAD;
   return PV_OK;
 }
 

@@ -13,6 +13,7 @@
 // per-signature algorithms live in pv_verify_core.h.
 #include <hip/hip_runtime.h>
 #include "pv_verify_core.h"
+#include "pv_quad.h"
 #include "pv_sha256.h"
 #include "pv_kernels.h"
 
@@ -543,6 +544,62 @@ hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_
   if (blocks * 64 > scratch_lanes) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_curve_lat, dim3((uint32_t)blocks), dim3(64), 0, s, pk, sig, dig, rec, btab, bw, scratch,
                      verdict, reinterpret_cast<unsigned long long*>(bitmap), n);
+  return hipGetLastError();
+}
+
+// k_curve_quad: the latency kernel (default for batches up to PV_LAT_MAX).
+// Signature i runs on the 8 lanes 8i..8i+7: side 0 (+-A and s'_lo B) on the
+// quad 8i..8i+3, side 1 (-R and s'_hi 2^128 B) on 8i+4..8i+7, each point's
+// four coordinates on the four lanes of its quad (pv_quad.h): a doubling is
+// one squaring + one multiply per lane, an addition two multiplies, so the
+// serial chain is ~1/2.5 of k_curve_lat's.  Deferred records (~0.2 %) take
+// the same kernel in their full-length form (64 windows of h on side 0, -R on
+// side 1), so no lane ever waits for a one-lane fallback.  Side 1 hands its
+// point to side 0 (cached form) through one lane shuffle; side 0 tests the
+// sum for the identity.  Tables: one 9-entry cached table per quad in LDS
+// (16 quads x 1440 B per block).  The bitmap (zeroed by k_lattice) takes one
+// 8-bit OR per block.
+__global__ __launch_bounds__(64) void k_curve_quad(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                                   const uint32_t* __restrict__ rec, const uint32_t* __restrict__ bw,
+                                                   uint8_t* __restrict__ verdict, unsigned long long* __restrict__ bitmap,
+                                                   uint64_t n) {
+  __shared__ uint32_t tabs[16 * QTAB_WORDS];
+  const int t = (int)threadIdx.x;
+  const int side = (t >> 2) & 1;
+  const QRole q = qrole_of((uint32_t)t & 3u);
+  const uint64_t i = (uint64_t)blockIdx.x * 8 + (uint64_t)(t >> 3);
+  const uint64_t ic = i < n ? i : n - 1;   // lanes past the batch run on the last record (results dropped)
+  const uint32_t* r = rec + HREC_WORDS * ic;
+  const uint32_t st = r[HREC_FLAGS] & 0xffu;
+  qfe Q;
+  const bool ok = q_side(Q, pk + 32 * ic, sig + 64 * ic, r, side, tabs + (t >> 2) * QTAB_WORDS,
+                         side ? bw + 4 * BW_TABLE : bw, q);
+  qfe e, e1;
+  q_to_cached(e, Q, q);
+#pragma unroll
+  for (int k = 0; k < 10; ++k) e1.l[0].v[k] = __shfl_xor(e.l[0].v[k], 4, 64);   // side 1 -> side 0
+  const bool ok1 = __shfl_xor(ok ? 1 : 0, 4, 64) != 0;
+  const bool id = q_sum_is_identity(Q, e1, q);
+  const bool v = (st == HS_HALF || st == HS_DEFER) && ok && ok1 && id;
+  const bool mine = side == 0 && (t & 3) == 0 && i < n;
+  if (mine) verdict[i] = v ? 1 : 0;
+  const uint64_t ball = __ballot(mine && v);   // bits 8k: signature blockIdx.x * 8 + k
+  if (t == 0 && ball) {
+    uint64_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bits |= ((ball >> (8 * k)) & 1ull) << k;
+    const uint64_t i0 = (uint64_t)blockIdx.x * 8;
+    atomicOr(&bitmap[i0 >> 6], (unsigned long long)(bits << (i0 & 63)));
+  }
+}
+
+hipError_t launch_curve_quad(const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, const uint32_t* bw,
+                             uint8_t* verdict, uint64_t* bitmap, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + 7) / 8;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_curve_quad, dim3((uint32_t)blocks), dim3(64), 0, s, pk, sig, rec, bw, verdict,
+                     reinterpret_cast<unsigned long long*>(bitmap), n);
   return hipGetLastError();
 }
 

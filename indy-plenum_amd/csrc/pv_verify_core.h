@@ -928,6 +928,7 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
 // (HS_NONE: rejected before the curve, HS_HALF, HS_DEFER) | c_neg << 8.
 constexpr int HREC_WORDS = 20;
 constexpr int HREC_C = 0, HREC_D = 5, HREC_S = 10, HREC_FLAGS = 18;
+constexpr int HREC_H = 0;   // deferred records: h's 64 offset nibbles over words 0..7 (S at HREC_S)
 constexpr int HALF_LANE_WORDS = 2 * AT_WORDS;   // tables of +-A and -R
 
 // pre = the hash stage's pre-check verdict; dig = SHA-512(R||A||M)
@@ -936,14 +937,15 @@ PV_HD uint32_t lattice_one(uint32_t* rec, bool pre, const uint32_t* dig, const u
   bool c_neg = false;
   if (pre) {
     st = HS_DEFER;
+    uint32_t h[8];
+    {
+      uint32_t x[16];
+      load8(x, reinterpret_cast<const uint8_t*>(dig));
+      load8(x + 8, reinterpret_cast<const uint8_t*>(dig + 8));
+      sc_reduce64(h, x);  // h = SHA-512(R||A||M) mod L (App. C.2 step 5)
+    }
     if (!force_full) {
-      uint32_t h[8], c[HS_WORDS], d[HS_WORDS];
-      {
-        uint32_t x[16];
-        load8(x, reinterpret_cast<const uint8_t*>(dig));
-        load8(x + 8, reinterpret_cast<const uint8_t*>(dig + 8));
-        sc_reduce64(h, x);  // h = SHA-512(R||A||M) mod L (App. C.2 step 5)
-      }
+      uint32_t c[HS_WORDS], d[HS_WORDS];
       st = half_scalars(c, d, c_neg, h);
       if (st == HS_HALF) {
         uint32_t S[8], sp[8];
@@ -959,6 +961,20 @@ PV_HD uint32_t lattice_one(uint32_t* rec, bool pre, const uint32_t* dig, const u
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) rec[HREC_S + k] = sp[k];
+      }
+    }
+    if (st == HS_DEFER) {
+      // full-length record (the lane-quad kernel's deferred form): h in signed
+      // radix-16 offset form (64 nibbles over words 0..7) and S in the signed
+      // radix-2^16 offset form of s'.  k_curve_half re-reads the digest instead.
+      uint32_t S[8], hp[8];
+      load8(S, sig + 32);
+      sc_add_pattern(hp, h, 0x88888888u);
+      sc_add_pattern(S, S, HALF_S_PATTERN);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        rec[HREC_H + k] = hp[k];
+        rec[HREC_S + k] = S[k];
       }
     }
   }

@@ -65,6 +65,7 @@ SIGNATURES = [
     ('pv_curve_stats', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)]),
     ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_set_lat_max', ctypes.c_int, [ctypes.c_uint64]),
+    ('pv_set_lat_kernel', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
     ('pv_kernel_timing', ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
@@ -93,9 +94,18 @@ LAT_MAX_DEFAULT = 2048   # PV_LAT_MAX in csrc/pv_api.cpp
 
 
 def set_lat_max(max_signatures):
-    """Largest generic batch that runs the latency-mode curve kernel (lane pairs
+    """Largest generic batch that runs the latency-mode curve kernel (8 lanes
     per signature) on every initialised device; 0 disables (pv_set_lat_max)."""
     _check('pv_set_lat_max', load().pv_set_lat_max(int(max_signatures)))
+
+
+LAT_KERNELS = {'quad': 0, 'pair': 1}   # PV_LAT_QUAD / PV_LAT_PAIR
+
+
+def set_lat_kernel(name):
+    """Latency kernel on every initialised device: 'quad' (default, lane quads
+    per point) or 'pair' (the lane-pair kernel, A/B) (pv_set_lat_kernel)."""
+    _check('pv_set_lat_kernel', load().pv_set_lat_kernel(LAT_KERNELS[name]))
 
 
 STAGING_MODES = {0: 'pinned', 1: 'pageable'}   # PV_STAGING_PINNED / _PAGEABLE

@@ -66,10 +66,11 @@ def test_c2_full_size_properties(torch_dev):
 
 
 def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
-    """The half-size path (default; throughput kernel and the latency-mode
-    lane-pair kernel), every record through its full-length tasks
-    (PV_CURVE_MODE=full) and the grouped kernel give identical verdicts and
-    bitmaps on a 200k C2-shaped batch and on every fixture; the half path's
+    """The half-size path (default; throughput kernel and both latency-mode
+    kernels: lane quads and lane pairs), every record through its full-length
+    form (PV_CURVE_MODE=full: the throughput kernel's full-length tasks and the
+    quad kernel's deferred form) and the grouped kernel give identical verdicts
+    and bitmaps on a 200k C2-shaped batch and on every fixture; the half path's
     deferred records really ran."""
     from plenum_gpu import _native as nat
     from plenum_gpu.device import SyntheticBatch
@@ -81,11 +82,13 @@ def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
     rows = split_sm(adversarial)
     r = raw_vectors
     try:
-        for mode in ('half', 'half_lat', 'full', 'grouped'):
-            # half: one lane per signature everywhere; half_lat: lane pairs for
-            # the 200k batch and every fixture
-            nat.set_lat_max(1 << 20 if mode == 'half_lat' else 0)
-            mode = 'half' if mode == 'half_lat' else mode
+        for mode in ('half', 'half_quad', 'half_pair', 'full', 'full_quad', 'grouped'):
+            # half/full: one lane per signature everywhere; *_quad / *_pair: the
+            # latency kernels for the 200k batch and every fixture
+            lat = mode.split('_')[1] if '_' in mode else None
+            nat.set_lat_max(1 << 20 if lat else 0)
+            nat.set_lat_kernel(lat or 'quad')
+            mode = mode.split('_')[0]
             nat.set_curve_mode(mode)
             b.bitmap.fill_(-1)     # the half path must clear it itself
             v = b.verify().cpu().numpy().astype(bool)
@@ -95,17 +98,32 @@ def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
                 assert 0 < deferred < n // 100      # ~0.2 % of random h
             elif mode == 'full':
                 assert deferred == int((~tamper).sum()) or deferred >= n * 0.9
-            assert (v == ~tamper).all(), mode
+            assert (v == ~tamper).all(), (mode, lat)
             bits = np.unpackbits(b.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
-            assert (bits == v).all(), mode
+            assert (bits == v).all(), (mode, lat)
             got = nat.verify_batch_arrays(r['pk'], r['sig'], r['blob'], r['off'])
-            assert (got == r['verdict'].astype(bool)).all(), mode
+            assert (got == r['verdict'].astype(bool)).all(), (mode, lat)
             got = verify_signed_batch([(pk, sm) for _, pk, sm, _ in rows])
             wrong = [rows[k][0] for k in range(len(rows)) if got[k] != rows[k][3]]
-            assert not wrong, (mode, wrong)
+            assert not wrong, (mode, lat, wrong)
     finally:
         nat.set_curve_mode('half')
         nat.set_lat_max(nat.LAT_MAX_DEFAULT)
+        nat.set_lat_kernel('quad')
+
+
+def test_latency_kernel_small_batches(torch_dev, raw_vectors):
+    """Looper-pass sizes through the default latency kernel (lane quads):
+    ragged batch sizes around the 8-signatures-per-block grid, each checked
+    against the libsodium verdicts of the raw-vector fixture."""
+    from plenum_gpu import _native as nat
+    r = raw_vectors
+    off = r['off']
+    for start, n in ((0, 1), (5, 7), (11, 8), (100, 9), (200, 100), (1000, 1000), (17, 2048)):
+        o = off[start:start + n + 1]
+        blob = r['blob'][int(o[0]):int(o[-1])]
+        got = nat.verify_batch_arrays(r['pk'][start:start + n], r['sig'][start:start + n], blob, o - o[0])
+        assert (got == r['verdict'][start:start + n].astype(bool)).all(), (start, n)
 
 
 def test_kernel_timer(torch_dev):

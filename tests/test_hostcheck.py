@@ -209,6 +209,45 @@ def test_half_and_full_paths_agree_on_fixtures(hc, raw_vectors, adversarial):
         assert (got == want).all()
 
 
+
+def _run_quad(hc, pk, sig, blob, off, force_full):
+    n = len(pk)
+    v = np.zeros(n, np.uint8)
+    nd = ctypes.c_uint64()
+    b = orc.padded(blob)
+    hc.hc_btable((ctypes.c_uint32 * (8 * 129 * 32))())
+    hc.hc_reset_counts()
+    hc.hc_verify_batch_quad(_p(np.ascontiguousarray(pk)), _p(np.ascontiguousarray(sig)), _p(b),
+                            _p(np.ascontiguousarray(off)), ctypes.c_uint64(n), _p(v), int(force_full), ctypes.byref(nd))
+    _, bad = counts(hc)
+    assert bad == 0, 'a field-multiply input exceeded the LOOSE bound'
+    return v.astype(bool), nd.value
+
+
+def test_lane_quad_schedule_on_fixtures(hc, raw_vectors, adversarial):
+    """The latency kernel's lane-quad schedule (k_curve_quad, pv_quad.h) with the
+    four lanes of a quad emulated in lockstep: every raw-vector and adversarial
+    verdict, half-size records and every record in its deferred (full-length)
+    form, every field-multiply input bound-checked."""
+    r = raw_vectors
+    sel = np.arange(0, len(r['verdict']), 7)
+    msgs = [r['blob'][int(r['off'][i]):int(r['off'][i + 1])].tobytes() for i in sel]
+    off = np.zeros(len(sel) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    blob = np.frombuffer(b''.join(msgs), np.uint8)
+    want = r['verdict'][sel].astype(bool)
+    for force in (False, True):
+        got, nd = _run_quad(hc, r['pk'][sel], r['sig'][sel], blob, off, force)
+        assert (got == want).all()
+        if force:
+            assert nd >= int(want.sum())
+    pk, sig, blob, off, want = _adv_arrays(adversarial)
+    for force in (False, True):
+        got, _ = _run_quad(hc, pk, sig, blob, off, force)
+        wrong = np.nonzero(got != want)[0]
+        assert len(wrong) == 0, wrong
+
+
 L8 = 8 * L
 PAT33 = int('8' * 33, 16)
 

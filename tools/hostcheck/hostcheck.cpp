@@ -54,6 +54,7 @@ static void hc_check_sq(const uint32_t* f) {
 
 #include "../../indy-plenum_amd/csrc/pv_verify_core.h"
 #include "../../indy-plenum_amd/csrc/pv_sha256.h"
+#include "../../indy-plenum_amd/csrc/pv_quad.h"
 
 using namespace pv;
 
@@ -151,6 +152,34 @@ void hc_verify_batch_mode(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
     } else if (st == HS_DEFER) {
       ok = verify_full_one(pk + 32 * i, sig + 64 * i, h, lane, g_btab);
       ++nd;
+    }
+    verdict[i] = ok ? 1 : 0;
+  }
+  if (n_deferred) *n_deferred = nd;
+}
+
+// verdicts with the latency kernel's algorithm (k_curve_quad: each side of
+// the lane-pair split on a lane QUAD, emulated here with the four lanes in
+// lockstep; deferred records take the quad's full-length form)
+void hc_verify_batch_quad(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
+                          uint8_t* verdict, int force_full, uint64_t* n_deferred) {
+  ensure_btab();
+  static uint32_t tab0[QTAB_WORDS], tab1[QTAB_WORDS];
+  uint32_t rec[HREC_WORDS];
+  uint64_t nd = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t h[16];
+    const bool pre = hash_one(h, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+    const uint32_t st = lattice_one(rec, pre, h, sig + 64 * i, force_full != 0);
+    bool ok = false;
+    if (st == HS_HALF || st == HS_DEFER) {
+      qfe Q0, Q1, e1;
+      const QRole qr = qrole_of(0);   // (the emulation gives lane j role j)
+      const bool ok0 = q_side(Q0, pk + 32 * i, sig + 64 * i, rec, 0, tab0, g_bw, qr);
+      const bool ok1 = q_side(Q1, pk + 32 * i, sig + 64 * i, rec, 1, tab1, g_bw + 4 * BW_TABLE, qr);
+      q_to_cached(e1, Q1, qr);
+      ok = ok0 && ok1 && q_sum_is_identity(Q0, e1, qr);
+      nd += st == HS_DEFER;
     }
     verdict[i] = ok ? 1 : 0;
   }
