@@ -46,7 +46,7 @@ int fail(int code, const char* fmt, ...) {
 #define PV_HOST_CHUNKS 8
 #define PV_HOST_CHUNK_MIN 32768
 // generic batches of at most this many signatures run the latency-mode curve
-// kernel (k_curve_quad: lane quads per point); PV_LAT_MAX env overrides (0 disables)
+// kernel (k_verify_quad: one launch, lane quads per point); PV_LAT_MAX env overrides (0 disables)
 #define PV_LAT_MAX 2048
 // shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
 #define PV_DEDUP_SAMPLE_MIN 262144
@@ -310,7 +310,7 @@ struct Device {
   int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
   size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
   uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; PV_LAT_MAX env (0 = off)
-  bool lat_quad = true;              // latency kernel: k_curve_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
+  bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
   PinBuf pin[2];
   std::shared_ptr<GatherPool> pool = std::make_shared<GatherPool>();  // host gather threads
   PinBuf vout;  // page-locked verdicts of the shard (D2H target; copied to the caller after the drain)
@@ -522,9 +522,20 @@ uint64_t* stage_bitmap(Workspace& w, uint64_t* bitmap, uint64_t n, int& rc) {
   return w.bitmap.p;
 }
 
+// small generic batches: the whole verify is one k_verify_quad launch
+bool lat_fused(const Device& d, const uint32_t* ktab, uint64_t n) {
+  return !ktab && d.mode != CurveMode::Grouped && n <= d.lat_max && d.lat_quad;
+}
+
 int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                  const uint64_t* off, uint64_t n, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
                  const uint32_t* kidx) {
+  if (lat_fused(d, ktab, n)) {
+    // k_verify_quad runs the whole verify; only the deferred counter is reset
+    HIP_OK(w.qc.ensure(2));
+    HIP_OK(hipMemsetAsync(w.qc.p, 0, sizeof(unsigned long long), s));
+    return PV_OK;
+  }
   HIP_OK(w.h.ensure(n * 16));
   HIP_OK(w.pre.ensure(n));
   HIP_OK(w.counter.ensure(1));
@@ -545,12 +556,14 @@ int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig,
   return PV_OK;
 }
 
-int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, uint64_t n, uint8_t* verdict,
-                  uint64_t* bm, hipStream_t s, const uint32_t* ktab, const uint32_t* kidx) {
+int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
+                  const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
+                  const uint32_t* kidx) {
   const bool half = !ktab && d.mode != CurveMode::Grouped;
-  if (half && n <= d.lat_max && d.lat_quad) {
-    // small batch: 8 lanes per signature, each point on a lane quad
-    HIP_OK(pv::launch_curve_quad(pk, sig, w.hrec.p, d.bw.p, verdict, bm, n, s));
+  if (lat_fused(d, ktab, n)) {
+    // small batch: one launch, 8 lanes per signature (each point on a lane
+    // quad) plus one hashing lane per signature in a second wave
+    HIP_OK(pv::launch_verify_quad(pk, sig, blob, off, n, d.bw.p, verdict, bm, w.qc.p, d.mode == CurveMode::Full, s));
     w.half_ran = true;
     d.last_ws = (int)(&w - d.ws);
   } else if (half && n <= d.lat_max) {
@@ -602,7 +615,7 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
   // the "hash" interval also holds the scalar stage of the half-size path
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (lev) HIP_OK(hipEventRecord(lev[1], s));
-  rc = enqueue_curve(d, w, pk, sig, n, verdict, bm, s, ktab, kidx);
+  rc = enqueue_curve(d, w, pk, sig, blob, off, n, verdict, bm, s, ktab, kidx);
   if (rc) return rc;
   if (lev) HIP_OK(hipEventRecord(lev[2], s));
   if (timed) {

@@ -66,10 +66,12 @@ constexpr int ATAB_LAT_WORDS = 9 * 40;
 hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, const uint32_t* rec,
                             const uint32_t* btab, const uint32_t* bw, uint32_t* scratch, uint64_t scratch_lanes,
                             uint8_t* verdict, uint64_t* bitmap, uint64_t n, hipStream_t s);
-// latency mode, default: lane quads per point (8 lanes per signature; deferred
-// records in the same launch), tables in LDS
-hipError_t launch_curve_quad(const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, const uint32_t* bw,
-                             uint8_t* verdict, uint64_t* bitmap, uint64_t n, hipStream_t s);
+// latency mode in one launch: pre-checks + hash + scalar stage (one wave) and
+// the lane-quad curve stage (another) per block of 8 signatures; *dcount +=
+// the deferred records (caller zeroes it); the bitmap needs no zeroing
+hipError_t launch_verify_quad(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
+                              const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap, unsigned long long* dcount,
+                              bool force_full, hipStream_t s);
 hipError_t launch_lattice(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, uint8_t* pre, uint64_t n,
                           uint32_t* rec, uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks,
                           uint64_t* bitmap, bool force_full, hipStream_t s);

@@ -547,33 +547,58 @@ hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_
   return hipGetLastError();
 }
 
-// k_curve_quad: the latency kernel (default for batches up to PV_LAT_MAX).
-// Signature i runs on the 8 lanes 8i..8i+7: side 0 (+-A and s'_lo B) on the
-// quad 8i..8i+3, side 1 (-R and s'_hi 2^128 B) on 8i+4..8i+7, each point's
-// four coordinates on the four lanes of its quad (pv_quad.h): a doubling is
-// one squaring + one multiply per lane, an addition two multiplies, so the
-// serial chain is ~1/2.5 of k_curve_lat's.  Deferred records (~0.2 %) take
-// the same kernel in their full-length form (64 windows of h on side 0, -R on
-// side 1), so no lane ever waits for a one-lane fallback.  Side 1 hands its
-// point to side 0 (cached form) through one lane shuffle; side 0 tests the
-// sum for the identity.  Tables: one 9-entry cached table per quad in LDS
-// (16 quads x 1440 B per block).  The bitmap (zeroed by k_lattice) takes one
-// 8-bit OR per block.
-__global__ __launch_bounds__(64) void k_curve_quad(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
-                                                   const uint32_t* __restrict__ rec, const uint32_t* __restrict__ bw,
-                                                   uint8_t* __restrict__ verdict, unsigned long long* __restrict__ bitmap,
-                                                   uint64_t n) {
+// k_verify_quad: the whole verify of a small batch in ONE launch (latency
+// mode: pre-checks, SHA-512(R||A||M), the scalar stage and the lane-quad
+// curve stage).  A block of 128 threads takes 8 signatures: wave 1 (one lane
+// per signature) runs the pre-checks, the hash and the lattice stage into an
+// LDS record while wave 0 (8 lanes per signature, lane quads) decodes -A and
+// -R and builds their tables, which do not depend on the scalars; after one
+// barrier wave 0 runs the windows.  Replaces 2 memsets + k_hash + k_lattice +
+// the curve launch: the serial one-lane hash and lattice chains (~25 + 40 us
+// per call) run under the decompressions.  Verdict bits are stored as the
+// block's byte of the bitmap (8 signatures), so nothing needs zeroing; the
+// deferred count (pv_curve_stats) is added to *dcount (zeroed by the caller).
+__global__ __launch_bounds__(128) void k_verify_quad(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+                                                     const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+                                                     uint64_t n, const uint32_t* __restrict__ bw,
+                                                     uint8_t* __restrict__ verdict, uint8_t* __restrict__ bitmap_bytes,
+                                                     uint64_t bitmap_len, unsigned long long* __restrict__ dcount,
+                                                     int force_full) {
   __shared__ uint32_t tabs[16 * QTAB_WORDS];
+  __shared__ uint32_t recs[8 * HREC_WORDS];
   const int t = (int)threadIdx.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * 8;
   const int side = (t >> 2) & 1;
   const QRole q = qrole_of((uint32_t)t & 3u);
-  const uint64_t i = (uint64_t)blockIdx.x * 8 + (uint64_t)(t >> 3);
-  const uint64_t ic = i < n ? i : n - 1;   // lanes past the batch run on the last record (results dropped)
-  const uint32_t* r = rec + HREC_WORDS * ic;
-  const uint32_t st = r[HREC_FLAGS] & 0xffu;
+  const uint64_t i = i0 + (uint64_t)((t & 63) >> 3);
+  const uint64_t ic = i < n ? i : n - 1;   // lanes past the batch run on the last signature (results dropped)
   qfe Q;
-  const bool ok = q_side(Q, pk + 32 * ic, sig + 64 * ic, r, side, tabs + (t >> 2) * QTAB_WORDS,
-                         side ? bw + 4 * BW_TABLE : bw, q);
+  bool ok = false;
+  if (t >= 64) {
+    // wave 1: the scalar stage, lane k for signature i0 + k
+    const int k = t - 64;
+    uint32_t st = HS_NONE;
+    if (k < 8) {
+      uint32_t* r = recs + HREC_WORDS * k;
+      r[HREC_FLAGS] = HS_NONE;
+      const uint64_t j = i0 + (uint64_t)k;
+      if (j < n) {
+        uint32_t dig[16];
+        const bool pre = hash_one(dig, pk + 32 * j, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
+        st = lattice_one(r, pre, dig, sig + 64 * j, force_full != 0);
+      }
+    }
+    const uint64_t dm = __ballot(st == HS_DEFER);
+    if (k == 0 && dm) atomicAdd(dcount, (unsigned long long)__popcll(dm));
+  } else {
+    // wave 0: the points and their tables
+    ok = q_side_table(Q, pk + 32 * ic, sig + 64 * ic, side, tabs + (t >> 2) * QTAB_WORDS, q);
+  }
+  __syncthreads();
+  if (t >= 64) return;
+  const uint32_t* r = recs + HREC_WORDS * (t >> 3);
+  const uint32_t st = r[HREC_FLAGS] & 0xffu;
+  q_side_msm(Q, r, side, tabs + (t >> 2) * QTAB_WORDS, side ? bw + 4 * BW_TABLE : bw, q);
   qfe e, e1;
   q_to_cached(e, Q, q);
 #pragma unroll
@@ -583,23 +608,27 @@ __global__ __launch_bounds__(64) void k_curve_quad(const uint8_t* __restrict__ p
   const bool v = (st == HS_HALF || st == HS_DEFER) && ok && ok1 && id;
   const bool mine = side == 0 && (t & 3) == 0 && i < n;
   if (mine) verdict[i] = v ? 1 : 0;
-  const uint64_t ball = __ballot(mine && v);   // bits 8k: signature blockIdx.x * 8 + k
-  if (t == 0 && ball) {
-    uint64_t bits = 0;
+  const uint64_t ball = __ballot(mine && v);   // bits 8k: signature i0 + k
+  if (t == 0) {
+    uint32_t bits = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) bits |= ((ball >> (8 * k)) & 1ull) << k;
-    const uint64_t i0 = (uint64_t)blockIdx.x * 8;
-    atomicOr(&bitmap[i0 >> 6], (unsigned long long)(bits << (i0 & 63)));
+    for (int k = 0; k < 8; ++k) bits |= (uint32_t)((ball >> (8 * k)) & 1ull) << k;
+    bitmap_bytes[blockIdx.x] = (uint8_t)bits;
+    // the last block also clears the rest of the last bitmap word
+    if ((uint64_t)blockIdx.x + 1 == gridDim.x)
+      for (uint64_t b = (uint64_t)blockIdx.x + 1; b < bitmap_len; ++b) bitmap_bytes[b] = 0;
   }
 }
 
-hipError_t launch_curve_quad(const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, const uint32_t* bw,
-                             uint8_t* verdict, uint64_t* bitmap, uint64_t n, hipStream_t s) {
+hipError_t launch_verify_quad(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
+                              const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap, unsigned long long* dcount,
+                              bool force_full, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + 7) / 8;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_curve_quad, dim3((uint32_t)blocks), dim3(64), 0, s, pk, sig, rec, bw, verdict,
-                     reinterpret_cast<unsigned long long*>(bitmap), n);
+  const uint64_t bytes = (n + 63) / 64 * 8;
+  hipLaunchKernelGGL(k_verify_quad, dim3((uint32_t)blocks), dim3(128), 0, s, pk, sig, blob, off, n, bw, verdict,
+                     reinterpret_cast<uint8_t*>(bitmap), bytes, dcount, force_full ? 1 : 0);
   return hipGetLastError();
 }
 

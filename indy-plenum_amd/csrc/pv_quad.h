@@ -1,4 +1,4 @@
-// Lane-quad group arithmetic for the latency kernel (k_curve_quad).
+// Lane-quad group arithmetic for the latency kernel (k_verify_quad).
 //
 // Plenum verifies at most 100 client or 1,000 node messages per Looper pass
 // (stp_core/config.py:32-33), so a pass's batch is a few waves: its latency is
@@ -265,25 +265,30 @@ PV_HD int q_digit(const uint32_t dw[8], int w) { return (int)((pick8(dw, w >> 3)
 
 // One side of the quad verdict (the lane-pair split of k_curve_lat, each
 // side now on a quad):
-//   side 0: Q = k (+-A) + b B,       k = |c| (33 windows) or h (deferred: 64)
+//   side 0: Q = c (-A) + b B,         c = the signed |c| (33 windows) or h (deferred: 64)
 //   side 1: Q = k (-R) + b (2^128 B), k = d or, deferred, 1
 // with b = s'_lo / s'_hi (S_lo / S_hi when deferred), so that
 // Q0 + Q1 = s' B + c (-A) + d (-R) (half-size) or S B - h A - R (deferred):
-// the identity iff libsodium accepts (pv_lattice.h).  tab = the quad's table
-// (QTAB_WORDS); bt = this side's radix-2^16 base-point table.  Returns false
-// when the side's point does not decode (or R is not canonical).
-PV_HD bool q_side(qfe& Q, const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, int side, uint32_t* tab,
-                  const uint32_t* bt, const QRole& q) {
-  const bool defer = (rec[HREC_FLAGS] & 0xffu) == HS_DEFER;
+// the identity iff libsodium accepts (pv_lattice.h).  The sign of c is folded
+// into the digits (c (-A) = |c| (+A): every digit of side 0 negated), so the
+// point and its table do not depend on the scalar stage: q_side_table runs
+// before the record exists (k_verify_quad overlaps it with the hash).
+
+// decode side's point (-A, or -R with canonical y) and write its cached
+// multiples 0..8 to the quad table `tab` (QTAB_WORDS, each lane its
+// coordinate); Q = the point.  false = does not decode.
+PV_HD bool q_side_table(qfe& Q, const uint8_t* pk, const uint8_t* sig, int side, uint32_t* tab, const QRole& q) {
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < QL; ++j) {
     // every lane of the quad decodes the point (the chain is serial anyway)
+    uint32_t enc[8];
+    load8(enc, side ? sig : pk);
     ge_p3 P;
-    ok = side_point(P, pk, sig, rec, side);
+    const bool dec = ge_frombytes_negate(P, enc);
+    ok = dec && (side == 0 || y_is_canonical(enc));
     role_coord(Q.l[j], P, qrole(j, q));
   }
-  // table: cached multiples 0..8, each lane storing its coordinate
   qfe e1, e, acc;
   q_to_cached(e1, Q, q);
 #pragma unroll
@@ -299,6 +304,16 @@ PV_HD bool q_side(qfe& Q, const uint8_t* pk, const uint8_t* sig, const uint32_t*
     q_to_cached(e, acc, q);
     q_store_cached(tab + 40 * k, e, q);
   }
+  return ok;
+}
+
+// Horner over the side's windows from its record (tab from q_side_table,
+// bt = the side's radix-2^16 base-point table): Q = the side's sum
+PV_HD void q_side_msm(qfe& Q, const uint32_t* rec, int side, const uint32_t* tab, const uint32_t* bt,
+                      const QRole& q) {
+  const uint32_t flags = rec[HREC_FLAGS];
+  const bool defer = (flags & 0xffu) == HS_DEFER;
+  const bool cneg = side == 0 && (flags & 0x100u);   // c < 0: side 0's digits negated
   // digit words: side 0 = |c| (words 0..4) or h (0..7); side 1 = d (5..9) or 1,
   // aligned so that the top window's word sits in dw[7] (half-size records
   // start at window 32 = word 4); the words then shift up one per 8 windows
@@ -318,11 +333,13 @@ PV_HD bool q_side(qfe& Q, const uint8_t* pk, const uint8_t* sig, const uint32_t*
 #pragma unroll
   for (int k = 0; k < 4; ++k) sw[k] = rec[HREC_S + 4 * side + k];
   const int top = full0 ? 63 : 32;
+  qfe acc, e;
 #pragma unroll
   for (int j = 0; j < QL; ++j) role_p3_identity(acc.l[j], qrole(j, q));
   int dg = (int)((dw[7] >> (4 * (top & 7))) & 15u) - 8;
-  q_load_cached(e, tab + 40 * (dg < 0 ? -dg : dg), dg < 0, q);
-  q_add(acc, e, dg < 0, q);
+  bool ng = (dg < 0) != cneg;
+  q_load_cached(e, tab + 40 * (dg < 0 ? -dg : dg), ng, q);
+  q_add(acc, e, ng, q);
 #pragma unroll 1
   for (int w = top - 1; w >= 0; --w) {
     if ((w & 7) == 7) {
@@ -331,7 +348,8 @@ PV_HD bool q_side(qfe& Q, const uint8_t* pk, const uint8_t* sig, const uint32_t*
     }
     // this window's entries are fetched before its doublings
     dg = (int)((dw[7] >> (4 * (w & 7))) & 15u) - 8;
-    q_load_cached(e, tab + 40 * (dg < 0 ? -dg : dg), dg < 0, q);
+    ng = (dg < 0) != cneg;
+    q_load_cached(e, tab + 40 * (dg < 0 ? -dg : dg), ng, q);
     const bool bwin = (w & 3) == 0 && w < 32;
     int db = 0;
     qfe eb;
@@ -343,10 +361,16 @@ PV_HD bool q_side(qfe& Q, const uint8_t* pk, const uint8_t* sig, const uint32_t*
     }
 #pragma unroll 1
     for (int k = 0; k < 4; ++k) q_dbl(acc, q);
-    q_add(acc, e, dg < 0, q);
+    q_add(acc, e, ng, q);
     if (bwin) q_add(acc, eb, db < 0, q);
   }
   Q = acc;
+}
+
+PV_HD bool q_side(qfe& Q, const uint8_t* pk, const uint8_t* sig, const uint32_t* rec, int side, uint32_t* tab,
+                  const uint32_t* bt, const QRole& q) {
+  const bool ok = q_side_table(Q, pk, sig, side, tab, q);
+  q_side_msm(Q, rec, side, tab, bt, q);
   return ok;
 }
 

@@ -225,7 +225,7 @@ def _run_quad(hc, pk, sig, blob, off, force_full):
 
 
 def test_lane_quad_schedule_on_fixtures(hc, raw_vectors, adversarial):
-    """The latency kernel's lane-quad schedule (k_curve_quad, pv_quad.h) with the
+    """The latency kernel's lane-quad schedule (k_verify_quad, pv_quad.h) with the
     four lanes of a quad emulated in lockstep: every raw-vector and adversarial
     verdict, half-size records and every record in its deferred (full-length)
     form, every field-multiply input bound-checked."""

@@ -158,7 +158,7 @@ void hc_verify_batch_mode(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
   if (n_deferred) *n_deferred = nd;
 }
 
-// verdicts with the latency kernel's algorithm (k_curve_quad: each side of
+// verdicts with the latency kernel's algorithm (k_verify_quad: each side of
 // the lane-pair split on a lane QUAD, emulated here with the four lanes in
 // lockstep; deferred records take the quad's full-length form)
 void hc_verify_batch_quad(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
