@@ -232,6 +232,30 @@ def end_to_end(batch, dedup, reps=5):
                         (pk.nbytes + sig.nbytes + blob.nbytes + off.nbytes) / 1e6, batch.n, reps)}
 
 
+def small_batch_latency(batch, sizes=(1, 100, 1000), reps=20):
+    """Host-buffer call time of Plenum's per-pass batch sizes (stp_core/config.py:32-33:
+    <= 100 client / 1,000 node messages) on this rank's first signatures: the
+    one-launch latency kernel.  Median and min of `reps` calls."""
+    pk, sig = batch.pk.cpu().numpy(), batch.sig.cpu().numpy()
+    off = batch.off.cpu().numpy().astype(np.uint64)
+    blob = batch.blob.cpu().numpy()
+    want = ~batch.tamper.cpu().numpy().astype(bool)
+    out, mism = {}, 0
+    for n in sizes:
+        args = (pk[:n], sig[:n], blob[:int(off[n])], off[:n + 1])
+        got = nat.verify_batch_arrays(*args, device_mask=1 << batch.device.index)
+        mism += int((got != want[:n]).sum())
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            nat.verify_batch_arrays(*args, device_mask=1 << batch.device.index)
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        out[str(n)] = {'ms_median': round(ts[reps // 2] * 1e3, 3), 'ms_min': round(ts[0] * 1e3, 3)}
+    out['verdict_mismatches'] = mism
+    return out
+
+
 def main_c1(args):
     """C1: the Plenum request-authentication path end to end (host preprocessing
     + one GPU verify per batch) vs the same per-request path on libsodium."""
@@ -675,6 +699,8 @@ def main():
     if world == 1 and args.config == 'c2' and not args.no_e2e:
         out['end_to_end'] = end_to_end(batch, key_cache)
         mism += out['end_to_end']['verdict_mismatches']
+        out['small_batch_latency'] = small_batch_latency(batch)
+        mism += out['small_batch_latency']['verdict_mismatches']
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -327,6 +327,7 @@ struct Device {
   DevBuf<unsigned long long> counter;  // SHA-256 work queue
   // staging for host-memory calls
   DevBuf<uint8_t> pk, sig, blob, verdict, tamper;
+  DevBuf<uint8_t> stage;      // small host-buffer calls: device image of pinned slot 0 (run_small)
   DevBuf<uint64_t> off, batch_off;
   DevBuf<uint32_t> sender, votes;
   DevBuf<uint32_t> tflag, tbits;  // tally: out-of-range sender flag; staged voter bitmaps
@@ -466,7 +467,7 @@ void release_device(Device& d) {
   for (auto& w : d.ws) w.release();
   if (d.ws[1].stream) (void)hipStreamDestroy(d.ws[1].stream);
   for (auto& w : d.ws) w.stream = nullptr;
-  d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release();
+  d.pk.release(); d.sig.release(); d.blob.release(); d.verdict.release(); d.tamper.release(); d.stage.release();
   d.off.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release(); d.tflag.release(); d.tbits.release();
   d.ktab.release(); d.kidx.release(); d.kscr.release(); d.kscr2.release(); d.mk0.release(); d.mk1.release();
@@ -646,9 +647,67 @@ struct HostBatch {
 // the copy stream, and verified on workspace c & 1's stream (see the loop).
 // Verdicts come back through a page-locked buffer.  Returns after every verdict of the
 // shard is in hb.verdict (or on error, after the device has drained).
+// A shard of a Looper-pass size (m <= lat_max: the one-launch latency kernel).
+// The inputs are gathered into page-locked slot 0 in the layout off | pk | sig
+// | blob | 16 zero bytes, DMA'd with ONE copy into the device image `stage`,
+// verified by one k_verify_quad launch and the verdicts copied back, all on
+// workspace 0's stream (no copy stream, no cross-stream events).  Keys are
+// never deduplicated here: the latency kernel beats preparing them (same
+// verdicts).  Returns 1 when the shard does not fit the path (caller falls
+// back to the pipeline).
+uint64_t small_bytes(const HostBatch& hb, uint64_t s, uint64_t e) {
+  const uint64_t m = e - s;
+  return (m + 1) * 8 + m * 96 + (hb.off[e] - hb.off[s]) + 16;
+}
+
+int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
+  const uint64_t m = e - s;
+  HIP_OK(hipSetDevice(d.id));
+  Workspace& w = d.ws[0];
+  struct Drain {
+    Device& d;
+    ~Drain() {
+      (void)hipSetDevice(d.id);
+      (void)hipStreamSynchronize(d.ws[0].stream);
+    }
+  } drain{d};
+  const uint64_t b0 = hb.off[s], bytes = hb.off[e] - b0;
+  const size_t o_pk = (m + 1) * 8, o_sig = o_pk + m * 32, o_blob = o_sig + m * 64, total = small_bytes(hb, s, e);
+  if (d.pin[0].ensure(total) != hipSuccess || d.vout.ensure(m) != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  HIP_OK(d.stage.ensure(total));
+  HIP_OK(d.verdict.ensure(m));
+  uint8_t* base = d.pin[0].p;
+  std::atomic<bool> bad{false};
+  const CopyJob jobs[4] = {{base, reinterpret_cast<const uint8_t*>(hb.off + s), (m + 1) * 8, b0, true},
+                           {base + o_pk, hb.pk + 32 * s, m * 32},
+                           {base + o_sig, hb.sig + 64 * s, m * 64},
+                           {base + o_blob, hb.blob ? hb.blob + b0 : nullptr, bytes}};
+  d.pool->run(jobs, 4, d.copy_threads, &bad);
+  if (bad.load())
+    return fail(PV_EINVAL, "msg_off not monotone in [%llu, %llu]", (unsigned long long)s, (unsigned long long)e);
+  memset(base + o_blob + bytes, 0, 16);   // the hash reads aligned words past the last message
+  HIP_OK(hipMemcpyAsync(d.stage.p, base, total, hipMemcpyHostToDevice, w.stream));
+  const uint8_t* g = d.stage.p;
+  const int rc = enqueue_verify(d, w, g + o_pk, g + o_sig, g + o_blob, reinterpret_cast<const uint64_t*>(g), m,
+                                d.verdict.p, nullptr, w.stream, false, nullptr, nullptr);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(d.vout.p, d.verdict.p, m, hipMemcpyDeviceToHost, w.stream));
+  HIP_OK(hipStreamSynchronize(w.stream));
+  memcpy(hb.verdict + s, d.vout.p, m);
+  return PV_OK;
+}
+
 int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   const uint64_t m = e - s;
   if (m == 0) return PV_OK;
+  if (m <= d.lat_max && d.lat_quad && d.mode != CurveMode::Grouped && d.pinned &&
+      small_bytes(hb, s, e) <= d.pin_max) {
+    const int rc = run_small(d, hb, s, e);
+    if (rc != 1) return rc;
+  }
   HIP_OK(hipSetDevice(d.id));
   // on every exit (errors included) wait for the work that reads host memory
   struct Drain {

@@ -217,6 +217,12 @@ def test_host_offsets_checked_before_launch(nat):
             nat.verify_batch_arrays(pk, sig, blob, bad, dedup_keys=False)
         assert (nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=False) == want).all()
     nat.set_host_staging('pinned', 8, 8)
+    # a Looper-pass-sized call (one gather, one DMA, one launch: run_small)
+    small = off[:501].copy()
+    small[300] = small[299] - 1
+    with pytest.raises(nat.PlenumGpuError, match='monotone'):
+        nat.verify_batch_arrays(pk[:500], sig[:500], blob[:int(off[500])], small)
+    assert (nat.verify_batch_arrays(pk[:500], sig[:500], blob[:int(off[500])], off[:501]) == want[:500]).all()
 
 
 def test_host_staging_slot_cap(nat):
