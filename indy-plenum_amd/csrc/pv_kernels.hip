@@ -547,6 +547,11 @@ hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_
   return hipGetLastError();
 }
 
+// PV_QUAD_PHASE (timing variants only, wrong verdicts): 1 skips the hash +
+// lattice wave, 2 the decompressions + tables, 3 the windows
+#ifndef PV_QUAD_PHASE
+#define PV_QUAD_PHASE 0
+#endif
 // k_verify_quad: the whole verify of a small batch in ONE launch (latency
 // mode: pre-checks, SHA-512(R||A||M), the scalar stage and the lane-quad
 // curve stage).  A block of 128 threads takes 8 signatures: wave 1 (one lane
@@ -582,7 +587,7 @@ __global__ __launch_bounds__(128) void k_verify_quad(const uint8_t* __restrict__
       uint32_t* r = recs + HREC_WORDS * k;
       r[HREC_FLAGS] = HS_NONE;
       const uint64_t j = i0 + (uint64_t)k;
-      if (j < n) {
+      if (j < n && PV_QUAD_PHASE != 1) {
         uint32_t dig[16];
         const bool pre = hash_one(dig, pk + 32 * j, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
         st = lattice_one(r, pre, dig, sig + 64 * j, force_full != 0);
@@ -592,13 +597,13 @@ __global__ __launch_bounds__(128) void k_verify_quad(const uint8_t* __restrict__
     if (k == 0 && dm) atomicAdd(dcount, (unsigned long long)__popcll(dm));
   } else {
     // wave 0: the points and their tables
-    ok = q_side_table(Q, pk + 32 * ic, sig + 64 * ic, side, tabs + (t >> 2) * QTAB_WORDS, q);
+    if (PV_QUAD_PHASE != 2) ok = q_side_table(Q, pk + 32 * ic, sig + 64 * ic, side, tabs + (t >> 2) * QTAB_WORDS, q);
   }
   __syncthreads();
   if (t >= 64) return;
   const uint32_t* r = recs + HREC_WORDS * (t >> 3);
   const uint32_t st = r[HREC_FLAGS] & 0xffu;
-  q_side_msm(Q, r, side, tabs + (t >> 2) * QTAB_WORDS, side ? bw + 4 * BW_TABLE : bw, q);
+  if (PV_QUAD_PHASE != 3) q_side_msm(Q, r, side, tabs + (t >> 2) * QTAB_WORDS, side ? bw + 4 * BW_TABLE : bw, q);
   qfe e, e1;
   q_to_cached(e, Q, q);
 #pragma unroll
