@@ -268,7 +268,8 @@ int pv_set_curve_mode(uint32_t mode);
  * squaring + one multiply: small batches, where a few waves occupy the GPU,
  * finish ~2x sooner.  Deferred records run in the same kernel.  Larger
  * batches keep the one-lane-per-signature throughput kernel.  Verdicts are
- * identical.  Default 2048, env PV_LAT_MAX at pv_init; 0 disables. */
+ * identical.  Default 32768 (the measured crossover with the throughput path
+ * is between 32k and 64k signatures), env PV_LAT_MAX at pv_init; 0 disables. */
 int pv_set_lat_max(uint64_t max_signatures);
 /* Latency kernel: PV_LAT_QUAD (default, lane quads per point) or PV_LAT_PAIR
  * (the previous lane-pair kernel, one lane per point; A/B).  Env

@@ -47,7 +47,7 @@ int fail(int code, const char* fmt, ...) {
 #define PV_HOST_CHUNK_MIN 32768
 // generic batches of at most this many signatures run the latency-mode curve
 // kernel (k_verify_quad: one launch, lane quads per point); PV_LAT_MAX env overrides (0 disables)
-#define PV_LAT_MAX 2048
+#define PV_LAT_MAX 32768
 // shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
 #define PV_DEDUP_SAMPLE_MIN 262144
 // chunk gathers into the pinned staging ring use up to this many host threads

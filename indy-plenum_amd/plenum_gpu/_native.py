@@ -90,7 +90,7 @@ def set_curve_mode(name):
     _check('pv_set_curve_mode', load().pv_set_curve_mode(code))
 
 
-LAT_MAX_DEFAULT = 2048   # PV_LAT_MAX in csrc/pv_api.cpp
+LAT_MAX_DEFAULT = 32768   # PV_LAT_MAX in csrc/pv_api.cpp
 
 
 def set_lat_max(max_signatures):

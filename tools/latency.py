@@ -11,17 +11,20 @@ import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'indy-plenum_amd'))
 
 
+SIZES = [int(x) for x in os.environ.get('PV_LAT_SIZES', '1,16,100,256,1000,1024,2048,4096,8192,16384,32768,65536').split(',')]
+
+
 def main():
     from plenum_gpu import _native as nat
     from plenum_gpu.device import SyntheticBatch
     nat.ensure_init()
-    b = SyntheticBatch(0, 65536, 256, cfg=2, first=99)
+    b = SyntheticBatch(0, max(SIZES), 256, cfg=2, first=99)
     pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()
     off = b.off.cpu().numpy().astype(np.uint64)
     blob = b.blob.cpu().numpy()[:int(off[-1])]
     want = ~b.tamper.cpu().numpy().astype(bool)
     lat = os.environ.get('PV_LAT_MAX')
-    for n in (1, 16, 100, 256, 1000, 1024, 4096, 16384, 32768, 65536):
+    for n in SIZES:
         args = (pk[:n], sig[:n], blob[:int(off[n])], off[:n + 1])
         got = nat.verify_batch_arrays(*args, dedup_keys=False)
         ts = []
