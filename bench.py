@@ -108,6 +108,32 @@ def _traffic_per_launch():
         return None
 
 
+def _combined_issue(kernel_rate, peak):
+    """SURVEY.md 8(d)'s integer-ALU roofline, 1 / (W_mad/P_mad + W_valu/P_valu), for
+    the C2 curve kernel: W_valu = the non-MAD VALU lane-ops the kernel executes per
+    verify (rocprofv3 SQ_INSTS_VALU of the C2 launch minus its MAD instructions,
+    profiles/r02_curve_pmc.json), P_valu = 2 x the measured MAD ceiling (full-rate
+    32-bit VALU issues at twice the half-rate v_mad_u64_u32).  A secondary figure:
+    `frac` above prices the MAD work alone."""
+    path = os.path.join(REPO, 'profiles', 'r02_curve_pmc.json')
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        insts = float(d['kernels'][d['curve_kernel']]['SQ_INSTS_VALU'])
+        n, deferred = int(d['c2_signatures']), int(d['c2_deferred'])
+    except (OSError, KeyError, ValueError):
+        return None
+    mad_lane_ops = W_MAD_PER_VERIFY * (n - deferred) + W_MAD_FULL * deferred
+    w_valu = (insts * 64 - mad_lane_ops) / n
+    p_valu = 2 * peak
+    rate = 1.0 / (W_MAD_PER_VERIFY / peak + w_valu / p_valu)
+    return {'model': 'SURVEY.md 8(d): 1 / (W_mad/P_mad + W_valu/P_valu)', 'w_mad_per_verify': W_MAD_PER_VERIFY,
+            'w_valu_per_verify': round(w_valu), 'p_mad': round(peak / 1e12, 3), 'p_valu': round(p_valu / 1e12, 3),
+            'unit': 'T lane-ops/s', 'roofline_verifies_per_s': round(rate, 1),
+            'frac': round(kernel_rate / rate, 4),
+            'source': 'W_valu from rocprofv3 SQ_INSTS_VALU of the C2 curve launch (profiles/r02_curve_pmc.json)'}
+
+
 def cpu_baseline(batch, workload, seconds=1.5, sample=8192):
     """libsodium crypto_sign_verify_detached on the host cores over the first
     `sample` signatures of this rank's workload (copied to host)."""
@@ -682,7 +708,9 @@ def main():
                                   'note': 'curve MAD work per step / per-step time of the timed region (every kernel '
                                           'of the step charged to the curve)'},
                      'traffic': _traffic_per_launch() if (args.config, n) == ('c2', CONFIGS['c2']['n']) else None,
-                     'work_per_verify': wpv},
+                     'work_per_verify': wpv,
+                     'combined_issue': _combined_issue(n / (ms_curve * 1e-3), peak)
+                     if (args.config, n) == ('c2', CONFIGS['c2']['n']) and curve_mode == 'half' else None},
         'curve_mode': curve_mode if not key_cache else 'keyed',
         'schedule': 'pipelined: consecutive steps alternate over 2 streams + 2 verify workspaces/output sets '
                     '(step k + 1 starts while step k drains; all K steps complete inside the timed region)'
