@@ -308,6 +308,7 @@ struct Device {
   bool pinned = true;
   int copy_threads = PV_HOST_COPY_THREADS;
   int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
+  int first_pct = 50;                // first chunk, % of a regular one; PV_HOST_FIRST_PCT env (10..100)
   size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
   uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; PV_LAT_MAX env (0 = off)
   bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
@@ -389,6 +390,11 @@ int init_device(Device& d) {
   if (const char* t = getenv("PV_HOST_CHUNKS")) {
     d.host_chunks = atoi(t);
     if (d.host_chunks < 1 || d.host_chunks > 256) return fail(PV_EINVAL, "PV_HOST_CHUNKS must be in 1..256 (got %s)", t);
+  }
+  if (const char* t = getenv("PV_HOST_FIRST_PCT")) {
+    d.first_pct = atoi(t);
+    if (d.first_pct < 10 || d.first_pct > 100)
+      return fail(PV_EINVAL, "PV_HOST_FIRST_PCT must be in 10..100 (got %s)", t);
   }
   if (const char* t = getenv("PV_LAT_MAX")) {
     const long v = atol(t);
@@ -778,7 +784,7 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   size_t cap = 0;
   for (uint64_t hc = d.host_chunks;; hc *= 2) {
     const uint64_t reg = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + hc - 1) / hc);
-    const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg / 2));
+    const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg * (uint64_t)d.first_pct / 100));
     bounds.assign(1, 0);
     if (hc > 1 && first < m) bounds.push_back(first);
     const uint64_t rest = m - bounds.back();
