@@ -130,16 +130,20 @@ class NaclAuthNr(ClientAuthNr):
             cache = self._verdict_cache = _VerdictCache()
         return cache
 
-    def _check_one(self, vr, sig_decoded, ser):
-        raw = getattr(vr, 'raw_verkey', None)
-        if raw is not None:
-            hit = self._verdicts().take(raw, bytes(sig_decoded) + bytes(ser))
+    def _check_one(self, vr, sig_decoded, ser, item=None):
+        # item: the (raw pk, sig||ser) key the prefetch built for this entry
+        if item is None:
+            raw = getattr(vr, 'raw_verkey', None)
+            if raw is not None:
+                item = (raw, bytes(sig_decoded) + bytes(ser))
+        if item is not None:
+            hit = self._verdicts().take(*item)
             if hit is not None:
                 return hit
         return vr.verify(sig_decoded, ser)
 
     def authenticate_multi(self, msg: Dict, signatures: Dict[str, str], threshold: Optional[int] = None,
-                           verifier: Verifier = DidVerifier):
+                           verifier: Verifier = DidVerifier, _prepared=None):
         provided = len(signatures)
         if threshold is None:
             threshold = provided
@@ -149,16 +153,26 @@ class NaclAuthNr(ClientAuthNr):
         accepted = []
         rejected = {}
         for idr, sig in signatures.items():
-            try:
-                sig_decoded = base58.b58decode(sig)
-            except Exception as ex:
-                raise InvalidSignatureFormat from ex
-            ser = self.serializeForSig(msg, identifier=idr)
-            verkey = self.getVerkey(idr, msg)
-            if verkey is None:
-                raise CouldNotAuthenticate(idr)
-            vr = self._verifier(verifier, verkey, idr)
-            if self._check_one(vr, sig_decoded, ser):
+            # _prepared (authenticate_batch's replay): {idr: (sig_decoded, ser,
+            # verifier object, verdict-cache key)} for the entries whose decode, serialization and
+            # key resolution the batch prefetch already ran without raising --
+            # the same pure computations on the same objects; anything else is
+            # recomputed here in the reference order, raising where it raises
+            prep = _prepared.get(idr) if _prepared else None
+            item = None
+            if prep is not None:
+                sig_decoded, ser, vr, item = prep
+            else:
+                try:
+                    sig_decoded = base58.b58decode(sig)
+                except Exception as ex:
+                    raise InvalidSignatureFormat from ex
+                ser = self.serializeForSig(msg, identifier=idr)
+                verkey = self.getVerkey(idr, msg)
+                if verkey is None:
+                    raise CouldNotAuthenticate(idr)
+                vr = self._verifier(verifier, verkey, idr)
+            if self._check_one(vr, sig_decoded, ser, item):
                 accepted.append(idr)
                 if len(accepted) == threshold:
                     return accepted
@@ -178,10 +192,12 @@ class NaclAuthNr(ClientAuthNr):
         return serialize_msg_for_signing(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)
 
     # ------------------------------------------------------------ batching
-    def _signature_items(self, msg, signatures, verifier=DidVerifier):
+    def _signature_items(self, msg, signatures, verifier=DidVerifier, prepared=None):
         """Every (raw pk, sig||ser) the reference loop could verify for this
         request, in loop order; entries whose decode / key lookup would raise
-        are skipped (the replay raises them)."""
+        are skipped (the replay raises them).  `prepared` (dict) receives
+        {idr: (sig_decoded, ser, verifier object, item or None)} of the
+        entries computed."""
         items = []
         for idr, sig in (signatures or {}).items():
             try:
@@ -190,12 +206,15 @@ class NaclAuthNr(ClientAuthNr):
                 if verkey is None:
                     continue
                 vr = self._verifier(verifier, verkey, idr)
+                ser = self.serializeForSig(msg, identifier=idr)
             except Exception:
                 continue
             raw = getattr(vr, 'raw_verkey', None)
-            if raw is None:
-                continue
-            items.append((raw, bytes(sig_decoded) + bytes(self.serializeForSig(msg, identifier=idr))))
+            item = None if raw is None else (raw, bytes(sig_decoded) + bytes(ser))
+            if prepared is not None:
+                prepared[idr] = (sig_decoded, ser, vr, item)
+            if item is not None:
+                items.append(item)
         return items
 
     def prefetch(self, items):
@@ -298,8 +317,10 @@ class CoreAuthMixin:
         return serialize_msg_for_signing(msg, topLevelKeysToIgnore=topLevelKeysToIgnore)
 
     # ------------------------------------------------------------ batching
-    def verify_batch(self, reqs, verifier: Verifier = DidVerifier):
-        """Prefetch GPU verdicts for every signature of every request."""
+    def verify_batch(self, reqs, verifier: Verifier = DidVerifier, _views=None):
+        """Prefetch GPU verdicts for every signature of every request.
+        `_views` (authenticate_batch) receives {id(req): (to_serialize,
+        signatures, prepared entries)} for the replay."""
         items = []
         for req in reqs:
             try:
@@ -308,17 +329,36 @@ class CoreAuthMixin:
                 continue
             if not isinstance(signatures, dict):
                 continue
-            items.extend(self._signature_items(to_serialize, signatures, verifier))
+            prepared = {} if _views is not None else None
+            items.extend(self._signature_items(to_serialize, signatures, verifier, prepared))
+            if _views is not None:
+                _views[id(req)] = (to_serialize, signatures, prepared)
         self.prefetch(items)
         return len(items)
 
+    def _replay_reuses_prefetch(self):
+        # the replay calls authenticate_multi with the prefetch's values only
+        # when neither entry point is overridden (a subclass keeps its own path)
+        t = type(self)
+        return t.authenticate is CoreAuthMixin.authenticate and t.authenticate_multi is NaclAuthNr.authenticate_multi
+
     def authenticate_batch(self, reqs, threshold: Optional[int] = None, verifier: Verifier = DidVerifier):
-        """[identifiers list | SigningException/other exception] per request."""
-        self.verify_batch(reqs, verifier)
+        """[identifiers list | SigningException/other exception] per request.
+        One GPU pass for the batch, then the reference's per-request control
+        flow; the replay reuses the prefetch's signing view, decoded signature,
+        serialized message and key object of each request (computed from the
+        same objects by the same pure functions within this call)."""
+        views = {} if self._replay_reuses_prefetch() else None
+        self.verify_batch(reqs, verifier, _views=views)
         out = []
         for req in reqs:
             try:
-                out.append(self.authenticate(req, threshold=threshold, verifier=verifier))
+                v = views.get(id(req)) if views is not None else None
+                if v is not None:
+                    out.append(self.authenticate_multi(v[0], signatures=v[1], threshold=threshold, verifier=verifier,
+                                                       _prepared=v[2]))
+                else:
+                    out.append(self.authenticate(req, threshold=threshold, verifier=verifier))
             except Exception as ex:
                 out.append(ex)
         self.drop_prefetched()

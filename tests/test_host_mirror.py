@@ -106,3 +106,31 @@ def test_fixture_covers_every_outcome(plenum_requests):
     kinds = {c['core'].get('exc', 'ok') for c in plenum_requests['cases']}
     assert {'ok', 'InsufficientCorrectSignatures', 'InvalidSignatureFormat', 'CouldNotAuthenticate',
             'InvalidKey', 'InsufficientSignatures', 'MissingSignature'} <= kinds
+
+
+def test_batched_replay_respects_overrides(plenum_requests, oracle_backend):
+    """authenticate_batch's replay reuses the prefetch's per-request values only
+    for the stock entry points: a subclass overriding authenticate keeps its
+    own per-request path (every request goes through the override), with the
+    same outcomes as the stock class on the golden fixture."""
+    import copy
+    from plenum_gpu.client_authn import CoreAuthNr
+    fx = plenum_requests
+
+    class Counting(CoreAuthNr):
+        calls = 0
+
+        def authenticate(self, req_data, *a, **kw):
+            Counting.calls += 1
+            return super().authenticate(req_data, *a, **kw)
+
+    stock = CoreAuthNr(fx['write_types'], fx['query_types'], fx['action_types'], state=pc.DictState(fx['state_nyms']))
+    sub = Counting(fx['write_types'], fx['query_types'], fx['action_types'], state=pc.DictState(fx['state_nyms']))
+    for idr, vk in fx['registry'].items():
+        stock.addIdr(idr, vk)
+        sub.addIdr(idr, vk)
+    assert stock._replay_reuses_prefetch() and not sub._replay_reuses_prefetch()
+    reqs = [copy.deepcopy(c['req']) for c in fx['cases'] if c.get('threshold') is None]
+    a = [pc.outcome_core(x) for x in stock.authenticate_batch(copy.deepcopy(reqs))]
+    b = [pc.outcome_core(x) for x in sub.authenticate_batch(copy.deepcopy(reqs))]
+    assert a == b and Counting.calls == len(reqs)
