@@ -552,6 +552,11 @@ hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_
 #ifndef PV_QUAD_PHASE
 #define PV_QUAD_PHASE 0
 #endif
+// PV_QUAD_LDS_PAD (A/B variants only): extra LDS words per block, to cap the
+// blocks a CU holds
+#ifndef PV_QUAD_LDS_PAD
+#define PV_QUAD_LDS_PAD 0
+#endif
 // k_verify_quad: the whole verify of a small batch in ONE launch (latency
 // mode: pre-checks, SHA-512(R||A||M), the scalar stage and the lane-quad
 // curve stage).  A block of 128 threads takes 8 signatures: wave 1 (one lane
@@ -569,10 +574,11 @@ __global__ __launch_bounds__(128) void k_verify_quad(const uint8_t* __restrict__
                                                      uint8_t* __restrict__ verdict, uint8_t* __restrict__ bitmap_bytes,
                                                      uint64_t bitmap_len, unsigned long long* __restrict__ dcount,
                                                      int force_full) {
-  __shared__ uint32_t tabs[16 * QTAB_WORDS];
+  __shared__ uint32_t tabs[16 * QTAB_WORDS + PV_QUAD_LDS_PAD];
   __shared__ uint32_t recs[8 * HREC_WORDS];
   const int t = (int)threadIdx.x;
   const uint64_t i0 = (uint64_t)blockIdx.x * 8;
+  if (PV_QUAD_LDS_PAD && t == 0) tabs[16 * QTAB_WORDS] = 0;   // (keeps the padding allocated)
   const int side = (t >> 2) & 1;
   const QRole q = qrole_of((uint32_t)t & 3u);
   const uint64_t i = i0 + (uint64_t)((t & 63) >> 3);
