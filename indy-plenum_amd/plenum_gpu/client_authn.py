@@ -63,9 +63,12 @@ def get_target_verkey(req: dict):
 
 
 class _VerdictCache:
-    """(raw pk, sig||msg) -> verdict, filled by a batch prefetch and consumed
-    by the per-request replay.  Bounded: a prefetch that would grow it past
-    MAX_ITEMS first forgets every older verdict (a miss only costs a verify)."""
+    """(raw pk, sig||msg) -> verdict, filled by a batch prefetch and read by
+    the per-request replay until the batch ends (drop_prefetched).  A verdict
+    is a pure function of its key, so a repeated (pk, sig||msg) in one batch
+    reads the same entry instead of costing a verify of its own.  Bounded: a
+    prefetch that would grow it past MAX_ITEMS first forgets every older
+    verdict (a miss only costs a verify)."""
     MAX_ITEMS = 1 << 20
 
     def __init__(self):
@@ -78,7 +81,7 @@ class _VerdictCache:
             self._d[item] = bool(ok)
 
     def take(self, pk, sm):
-        return self._d.pop((pk, sm), None)
+        return self._d.get((pk, sm))
 
     def clear(self):
         self._d.clear()
