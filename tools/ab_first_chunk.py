@@ -29,6 +29,7 @@ def main():
         ts.append(time.perf_counter() - t0)
     ts.sort()
     print(json.dumps({'chunks': os.environ.get('PV_HOST_CHUNKS', '8'), 'first_pct': os.environ.get('PV_HOST_FIRST_PCT', '50'),
+                      'staging': os.environ.get('PV_HOST_STAGING', 'pinned'),
                       'ms_min': round(ts[0] * 1e3, 3), 'ms_median': round(ts[4] * 1e3, 3),
                       'mismatches': int((got != want).sum())}), flush=True)
 
