@@ -661,6 +661,30 @@ struct HostBatch {
 // never deduplicated here: the latency kernel beats preparing them (same
 // verdicts).  Returns 1 when the shard does not fit the path (caller falls
 // back to the pipeline).
+// [p, p + n) lies inside one page-locked host allocation (hipHostMalloc'd or
+// registered by the caller, e.g. torch pin_memory()), so the copy engine can
+// read it directly and the gather into the staging ring can be skipped
+bool host_locked(const void* p, size_t n) {
+  if (n == 0) return true;
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost) return false;
+  void* start = nullptr;
+  size_t size = 0;
+  hipDeviceptr_t dp = const_cast<void*>(p);
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, dp) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, dp) != hipSuccess || !start) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return static_cast<const char*>(p) >= static_cast<const char*>(start) &&
+         static_cast<const char*>(p) + n <= static_cast<const char*>(start) + size;
+}
+
 uint64_t small_bytes(const HostBatch& hb, uint64_t s, uint64_t e) {
   const uint64_t m = e - s;
   return (m + 1) * 8 + m * 96 + (hb.off[e] - hb.off[s]) + 16;
@@ -807,6 +831,10 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   }
   std::vector<uint64_t> offs;  // pageable staging: the shard's rebased offsets (read by in-flight copies)
   if (!pinned) offs.resize(m + 1);
+  // caller buffers already page-locked: DMA pk / sig / blob straight from them,
+  // only the offsets (rebased, checked) go through the staging ring
+  const bool direct = pinned && !keyed && host_locked(pk + 32 * s, m * 32) && host_locked(hb.sig + 64 * s, m * 64) &&
+                      host_locked(hb.blob ? hb.blob + b0 : nullptr, bytes);
   HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.copy));
   if (keyed) {
     HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
@@ -824,8 +852,8 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   static const bool trace = getenv("PV_HOST_TRACE") && getenv("PV_HOST_TRACE")[0] == '1';
   const auto tstart = std::chrono::steady_clock::now();
   auto us = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tstart).count(); };
-  if (trace) fprintf(stderr, "[pv host] dev %d shard %llu sigs: setup %.1f us, %zu chunks, pinned %d\n", d.id,
-                     (unsigned long long)m, us(), nch, (int)pinned);
+  if (trace) fprintf(stderr, "[pv host] dev %d shard %llu sigs: setup %.1f us, %zu chunks, pinned %d, direct %d\n", d.id,
+                     (unsigned long long)m, us(), nch, (int)pinned, (int)direct);
   // chunk c is verified on workspace c & 1 and its stream, so chunk c + 1's
   // kernels start while chunk c's curve grid drains.  (A separate prep stream
   // for every chunk's hash + lattice with three workspaces measured no better:
@@ -854,12 +882,14 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
                                {p_pk, src_pk, keyed ? 0 : mc * 32},
                                {p_sig, src_sig, mc * 64},
                                {p_blob, src_blob, cbytes}};
-      d.pool->run(jobs, 4, d.copy_threads, &bad);
+      d.pool->run(jobs, direct ? 1 : 4, d.copy_threads, &bad);
       if (trace) t_gather = us();
       src_off = p_off;
-      src_pk = p_pk;
-      src_sig = p_sig;
-      src_blob = p_blob;
+      if (!direct) {
+        src_pk = p_pk;
+        src_sig = p_sig;
+        src_blob = p_blob;
+      }
     } else {
       const CopyJob job{reinterpret_cast<uint8_t*>(offs.data() + c0), reinterpret_cast<const uint8_t*>(hb.off + s + c0),
                         (mc + 1) * 8, b0, true};

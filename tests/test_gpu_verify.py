@@ -199,6 +199,27 @@ def test_host_pipeline_multi_chunk(nat, shape):
         nat.set_host_staging('pinned', 8, 8)
 
 
+def test_host_page_locked_inputs_direct(nat):
+    """Caller buffers that are already page-locked (torch pin_memory()) are DMA'd
+    directly (no gather copy): verdicts of a multi-chunk shard == not tampered,
+    and a decreasing offset is still refused before any kernel reads it."""
+    import torch
+    from plenum_gpu.device import SyntheticBatch
+    b = SyntheticBatch(0, 131075, 256, cfg=2, first=4242)
+    off = b.off.cpu().numpy().astype(np.uint64)
+    t = [b.pk.cpu().pin_memory(), b.sig.cpu().pin_memory(), b.blob.cpu()[:int(off[-1])].pin_memory(),
+         torch.from_numpy(off.view(np.int64)).pin_memory()]
+    pk, sig, blob, loff = t[0].numpy(), t[1].numpy(), t[2].numpy(), t[3].numpy().view(np.uint64)
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    nat.set_host_staging('pinned', 8, 8)
+    got = nat.verify_batch_arrays(pk, sig, blob, loff, dedup_keys=False)
+    assert (got == want).all(), int((got != want).sum())
+    bad = loff.copy()
+    bad[90001] = bad[90000] - 1
+    with pytest.raises(nat.PlenumGpuError, match='monotone'):
+        nat.verify_batch_arrays(pk, sig, blob, bad, dedup_keys=False)
+
+
 def test_host_offsets_checked_before_launch(nat):
     """msg_off is validated chunk by chunk while it is gathered: a decreasing
     offset in the middle of a multi-chunk shard is PV_EINVAL (no kernel reads
