@@ -221,8 +221,8 @@ def _sodium_did_verifier():
 
 def end_to_end(batch, dedup, reps=5):
     """Host-buffer rate of pv_verify_batch on this rank's workload: pk/sig/M in
-    pageable host memory -> H2D (chunked, overlapped with the kernels) -> hash +
-    curve -> D2H verdicts.  SURVEY.md 8(d)'s second number; never `value`."""
+    pageable host memory -> H2D (chunked, overlapped with the kernels) -> one
+    fused verify launch per chunk + a deferred pass -> D2H verdicts.  SURVEY.md 8(d)'s second number; never `value`."""
     pk, sig = batch.pk.cpu().numpy(), batch.sig.cpu().numpy()
     off = batch.off.cpu().numpy().astype(np.uint64)
     blob = batch.blob.cpu().numpy()[:int(off[-1])]
@@ -268,9 +268,11 @@ def end_to_end(batch, dedup, reps=5):
                                    'note': 'the same call with the caller\'s buffers already page-locked (torch '
                                            'pin_memory()): pk / sig / blob DMA\'d directly, no gather copy'},
             'path': 'pv_verify_batch from pageable host numpy buffers ({:.0f} MB in, {} B out): chunks gathered by '
-                    'host threads into two page-locked slots, DMA on a copy stream overlapped with hash + curve '
-                    'kernels (chunks alternate over two compute streams), D2H verdicts through a page-locked '
-                    'buffer; 2 untimed calls, then mean of {} calls'.format(
+                    'host threads into two page-locked slots (leading chunks of 32k and 64k signatures), DMA on a '
+                    'copy stream overlapped with one fused pre-check + hash + lattice + curve launch per chunk '
+                    '(k_chunk_half; chunks alternate over two compute streams), one lane-quad pass over the '
+                    'deferred records, D2H verdicts through a page-locked buffer; 2 untimed calls, then mean '
+                    'of {} calls'.format(
                         (pk.nbytes + sig.nbytes + blob.nbytes + off.nbytes) / 1e6, batch.n, reps)}
 
 

@@ -277,6 +277,12 @@ int pv_set_lat_max(uint64_t max_signatures);
 #define PV_LAT_QUAD 0u
 #define PV_LAT_PAIR 1u
 int pv_set_lat_kernel(uint32_t kernel);
+/* Host-buffer chunks of generic batches above the latency size: 1 (default) =
+ * one fused launch per chunk (pre-checks + hash + scalar stage + half-size
+ * curve per 64-signature task) and one lane-quad pass over the deferred
+ * records; 0 = the device-resident schedule (hash, lattice, curve launches)
+ * per chunk.  Same verdicts.  Env PV_HOST_FUSED=0|1 at pv_init. */
+int pv_set_host_fused(int enable);
 int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 
 /* Live kernel timing of the verify calls themselves (bench.py's timed region):

@@ -41,10 +41,15 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-// host-buffer pipeline (pv_verify_batch): a shard runs as at most
-// PV_HOST_CHUNKS chunks of at least PV_HOST_CHUNK_MIN signatures
+// host-buffer pipeline (pv_verify_batch): a shard runs as leading ramp
+// chunks and then at most PV_HOST_CHUNKS chunks of at least PV_HOST_CHUNK_MIN
+// signatures
 #define PV_HOST_CHUNKS 8
 #define PV_HOST_CHUNK_MIN 32768
+// ramp: leading chunks of 32768, 65536, ... signatures (below a regular
+// chunk), so the first grid starts after a ~12 MB DMA (C2 end to end with
+// fused chunks 11.6 vs 12.1 ms, profiles/r02_ab_fused_chunking.jsonl)
+#define PV_HOST_RAMP 32768
 // generic batches of at most this many signatures run the latency-mode curve
 // kernel (k_verify_quad: one launch, lane quads per point); PV_LAT_MAX env overrides (0 disables)
 #define PV_LAT_MAX 32768
@@ -309,9 +314,19 @@ struct Device {
   int copy_threads = PV_HOST_COPY_THREADS;
   int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
   int first_pct = 50;                // first chunk, % of a regular one; PV_HOST_FIRST_PCT env (10..100)
+  // leading chunks r, 2r, 4r, ... below a regular chunk instead of one first
+  // chunk (PV_HOST_RAMP env; 0 = off, first_pct then sizes the first chunk)
+  uint64_t ramp = PV_HOST_RAMP;
   size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
   uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; PV_LAT_MAX env (0 = off)
   bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
+  // host-buffer chunks of generic batches: one k_chunk_half launch per chunk
+  // + one k_verify_quad_list pass for the deferred records; PV_HOST_FUSED=0:
+  // k_hash + k_lattice + k_curve_half per chunk (the device-resident schedule)
+  bool chunk_fused = true;
+  DevBuf<uint32_t> dl;               // shard indices deferred by k_chunk_half
+  DevBuf<unsigned long long> dlc;    // their count
+  hipEvent_t joined = nullptr;       // ws[1] drained into ws[0] (deferred pass)
   PinBuf pin[2];
   std::shared_ptr<GatherPool> pool = std::make_shared<GatherPool>();  // host gather threads
   PinBuf vout;  // page-locked verdicts of the shard (D2H target; copied to the caller after the drain)
@@ -383,6 +398,7 @@ int init_device(Device& d) {
   HIP_OK(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
   for (auto& e : d.staged) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&d.keys_ready, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&d.joined, hipEventDisableTiming));
   if (const char* m = getenv("PV_HOST_STAGING")) {
     if (!strcmp(m, "pageable")) d.pinned = false;
     else if (strcmp(m, "pinned") != 0) return fail(PV_EINVAL, "PV_HOST_STAGING must be pinned or pageable (got %s)", m);
@@ -396,10 +412,19 @@ int init_device(Device& d) {
     if (d.first_pct < 10 || d.first_pct > 100)
       return fail(PV_EINVAL, "PV_HOST_FIRST_PCT must be in 10..100 (got %s)", t);
   }
+  if (const char* t = getenv("PV_HOST_RAMP")) {
+    const long v = atol(t);
+    if (v != 0 && (v < 1024 || v > (1L << 20))) return fail(PV_EINVAL, "PV_HOST_RAMP must be 0 or in 1024..1048576 (got %s)", t);
+    d.ramp = (uint64_t)v;
+  }
   if (const char* t = getenv("PV_LAT_MAX")) {
     const long v = atol(t);
     if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_MAX must be in 0..1048576 (got %s)", t);
     d.lat_max = (uint64_t)v;
+  }
+  if (const char* t = getenv("PV_HOST_FUSED")) {
+    if (strcmp(t, "0") != 0 && strcmp(t, "1") != 0) return fail(PV_EINVAL, "PV_HOST_FUSED must be 0 or 1 (got %s)", t);
+    d.chunk_fused = t[0] == '1';
   }
   if (const char* m = getenv("PV_LAT_KERNEL")) {
     if (!strcmp(m, "pair")) d.lat_quad = false;
@@ -491,6 +516,9 @@ void release_device(Device& d) {
     if (e) (void)hipEventDestroy(e), e = nullptr;
   if (d.keys_ready) (void)hipEventDestroy(d.keys_ready);
   d.keys_ready = nullptr;
+  if (d.joined) (void)hipEventDestroy(d.joined);
+  d.joined = nullptr;
+  d.dl.release(); d.dlc.release();
   d.pin[0].release();
   d.pin[1].release();
   d.vout.release();
@@ -796,8 +824,10 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   HIP_OK(d.blob.ensure(bytes + 16));
   HIP_OK(d.off.ensure(m + 1));
   HIP_OK(d.verdict.ensure(m));
-  // chunk bounds: a short first chunk (half a regular one, >= PV_HOST_CHUNK_MIN)
-  // so the kernels start early, then the rest in equal chunks.  With pinned
+  // chunk bounds: short leading chunks so the kernels start early -- the
+  // ramp r, 2r, ... below a regular chunk (default), or with PV_HOST_RAMP=0
+  // one first chunk of first_pct % of a regular one (>= PV_HOST_CHUNK_MIN) --
+  // then the rest in equal chunks.  With pinned
   // staging the chunk count doubles until a chunk's inputs fit one
   // pin_max slot; a shard whose PV_HOST_CHUNK_MIN-signature chunks still do not
   // fit (or whose page-locked allocation fails) uses pageable staging.
@@ -810,7 +840,13 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     const uint64_t reg = std::max<uint64_t>(PV_HOST_CHUNK_MIN, (m + hc - 1) / hc);
     const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg * (uint64_t)d.first_pct / 100));
     bounds.assign(1, 0);
-    if (hc > 1 && first < m) bounds.push_back(first);
+    if (hc > 1 && d.ramp) {
+      // PV_HOST_RAMP=r: leading chunks of r, 2r, 4r, ... signatures (< a
+      // regular chunk), so the first kernels start after a short DMA
+      for (uint64_t r = d.ramp; r < reg && bounds.back() + r < m; r *= 2) bounds.push_back(bounds.back() + r);
+    } else if (hc > 1 && first < m) {
+      bounds.push_back(first);
+    }
     const uint64_t rest = m - bounds.back();
     const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>((rest + reg - 1) / reg, rest / PV_HOST_CHUNK_MIN));
     const uint64_t c0 = bounds.back();
@@ -836,6 +872,18 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   const bool direct = pinned && !keyed && host_locked(pk + 32 * s, m * 32) && host_locked(hb.sig + 64 * s, m * 64) &&
                       host_locked(hb.blob ? hb.blob + b0 : nullptr, bytes);
   HIP_OK(hipMemsetAsync(d.blob.p + bytes, 0, 16, d.copy));
+  // generic batches: one fused launch per chunk, deferred records listed for
+  // one lane-quad pass at the end (its count is zeroed on the copy stream,
+  // which every chunk's kernels wait for)
+  // (PV_CURVE_MODE=full: every record deferred, i.e. verified by the list pass)
+  const bool fused = !keyed && d.chunk_fused && d.mode != CurveMode::Grouped;
+  if (fused) {
+    if (m > 0xffffffffull) return fail(PV_EINVAL, "at most 2^32-1 signatures per device call");
+    HIP_OK(d.dl.ensure(m));
+    HIP_OK(d.dlc.ensure(1));
+    HIP_OK(hipMemsetAsync(d.dlc.p, 0, sizeof(unsigned long long), d.copy));
+    for (auto& w : d.ws) w.half_ran = false;   // pv_curve_stats describes device-resident calls
+  }
   if (keyed) {
     HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
     HIP_OK(d.kidx.ensure(m));
@@ -906,6 +954,18 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     HIP_OK(hipEventRecord(d.copied, d.copy));
     HIP_OK(hipStreamWaitEvent(w.stream, d.copied, 0));
     // blob base + shard-relative offsets: the hash kernel reads blob + off[i]
+    if (fused) {
+      HIP_OK(w.hrec.ensure(mc * pv::HSREC_WORDS));
+      HIP_OK(w.qc.ensure(2));
+      HIP_OK(w.scratch.ensure(d.scratch_words));
+      HIP_OK(pv::launch_chunk_half(d.pk.p + 32 * c0, d.sig.p + 64 * c0, d.blob.p, d.off.p + c0, mc, w.hrec.p, d.bw.p,
+                                   w.scratch.p, w.scratch.cap / pv::HALF_SCRATCH_WORDS, d.verdict.p + c0, d.dl.p,
+                                   d.dlc.p, c0, w.qc.p + 1, d.curve_half_blocks, d.mode == CurveMode::Full, w.stream));
+      if (trace)
+        fprintf(stderr, "[pv host] chunk %zu (%llu sigs): begin %.1f slot-free %.1f gathered %.1f enqueued %.1f us\n", c,
+                (unsigned long long)mc, t_begin, t_slot, t_gather, us());
+      continue;
+    }
     int rc = enqueue_verify(d, w, keyed ? d.pk.p : d.pk.p + 32 * c0, d.sig.p + 64 * c0, d.blob.p, d.off.p + c0, mc,
                             d.verdict.p + c0, nullptr, w.stream, false, nullptr, nullptr, keyed ? d.ktab.p : nullptr,
                             keyed ? d.kidx.p + c0 : nullptr);
@@ -915,6 +975,16 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     if (trace)
       fprintf(stderr, "[pv host] chunk %zu (%llu sigs): begin %.1f slot-free %.1f gathered %.1f enqueued %.1f us\n", c,
               (unsigned long long)mc, t_begin, t_slot, t_gather, us());
+  }
+  if (fused) {
+    // the deferred records of every chunk (ws[1]'s chunks joined into ws[0]),
+    // then all verdicts in one copy
+    Workspace& w0 = d.ws[0];
+    HIP_OK(hipEventRecord(d.joined, d.ws[1].stream));
+    HIP_OK(hipStreamWaitEvent(w0.stream, d.joined, 0));
+    HIP_OK(pv::launch_verify_quad_list(d.pk.p, d.sig.p, d.blob.p, d.off.p, d.dl.p, d.dlc.p, m, d.cu_count * 8, d.bw.p,
+                                       d.verdict.p, d.mode == CurveMode::Full, w0.stream));
+    HIP_OK(hipMemcpyAsync(pinned ? d.vout.p : hb.verdict + s, d.verdict.p, m, hipMemcpyDeviceToHost, w0.stream));
   }
   HIP_OK(hipStreamSynchronize(d.copy));
   for (auto& w : d.ws) HIP_OK(hipStreamSynchronize(w.stream));
@@ -1183,6 +1253,13 @@ int pv_set_curve_mode(uint32_t mode) {
     d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
     for (auto& w : d.ws) w.half_ran = false;
   }
+  return PV_OK;
+}
+
+int pv_set_host_fused(int enable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  for (auto& d : g_devs) d.chunk_fused = enable != 0;
   return PV_OK;
 }
 

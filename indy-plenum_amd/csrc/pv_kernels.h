@@ -72,6 +72,19 @@ hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_
 hipError_t launch_verify_quad(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n,
                               const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap, unsigned long long* dcount,
                               bool force_full, hipStream_t s);
+// host-buffer chunks: the whole half-size verify of a chunk in one persistent
+// launch (pre-checks + hash + lattice + curve per 64-signature task; rec =
+// HSREC_WORDS per signature, scratch as launch_curve_half); deferred records
+// are appended to dlist as base + i (*dcount, zeroed by the caller) and left
+// for launch_verify_quad_list, which verifies the listed indices (count read
+// on the device; max_count bounds the grid) with the lane-quad kernel
+hipError_t launch_chunk_half(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                             uint64_t n, uint32_t* rec, const uint32_t* bw, uint32_t* scratch, uint64_t scratch_lanes,
+                             uint8_t* verdict, uint32_t* dlist, unsigned long long* dcount, uint64_t base,
+                             unsigned long long* tasks, int blocks, bool force_full, hipStream_t s);
+hipError_t launch_verify_quad_list(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                                   const uint32_t* list, const unsigned long long* lcount, uint64_t max_count,
+                                   int blocks, const uint32_t* bw, uint8_t* verdict, bool force_full, hipStream_t s);
 hipError_t launch_lattice(const uint8_t* pk, const uint8_t* sig, const uint32_t* dig, uint8_t* pre, uint64_t n,
                           uint32_t* rec, uint32_t* dlist, unsigned long long* dcount, unsigned long long* tasks,
                           uint64_t* bitmap, bool force_full, hipStream_t s);

@@ -643,6 +643,145 @@ hipError_t launch_verify_quad(const uint8_t* pk, const uint8_t* sig, const uint8
   return hipGetLastError();
 }
 
+// k_verify_quad_list: k_verify_quad over a device-side LIST of signature
+// indices (the records k_chunk_half deferred), count in *lcount (known only
+// on the device): a fixed grid of blocks loops over groups of 8 entries, so
+// the launch needs no read-back.  Verdicts go to verdict[index]; no bitmap
+// (host-buffer calls return verdicts only).  The listed records are the
+// deferred ones, so most take the quad kernel's full-length form (64 windows
+// of h): ~0.4 ms per pass, about twice a half-size group.
+__global__ __launch_bounds__(128) void k_verify_quad_list(const uint8_t* __restrict__ pk,
+                                                          const uint8_t* __restrict__ sig,
+                                                          const uint8_t* __restrict__ blob,
+                                                          const uint64_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ list,
+                                                          const unsigned long long* __restrict__ lcount,
+                                                          const uint32_t* __restrict__ bw, uint8_t* __restrict__ verdict,
+                                                          int force_full) {
+  __shared__ uint32_t tabs[16 * QTAB_WORDS];
+  __shared__ uint32_t recs[8 * HREC_WORDS];
+  const int t = (int)threadIdx.x;
+  const uint64_t cnt = *lcount;
+  const int side = (t >> 2) & 1;
+  const QRole q = qrole_of((uint32_t)t & 3u);
+  for (uint64_t g = blockIdx.x; g * 8 < cnt; g += gridDim.x) {
+    const uint64_t e = g * 8 + (uint64_t)((t & 63) >> 3);
+    const uint64_t ic = list[e < cnt ? e : cnt - 1];   // lanes past the list repeat its last entry (dropped)
+    qfe Q;
+    bool ok = false;
+    if (t >= 64) {
+      const int k = t - 64;
+      if (k < 8) {
+        uint32_t* r = recs + HREC_WORDS * k;
+        r[HREC_FLAGS] = HS_NONE;
+        if (g * 8 + (uint64_t)k < cnt) {
+          const uint64_t j = list[g * 8 + (uint64_t)k];
+          uint32_t dig[16];
+          const bool pre = hash_one(dig, pk + 32 * j, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
+          (void)lattice_one(r, pre, dig, sig + 64 * j, force_full != 0);
+        }
+      }
+    } else {
+      ok = q_side_table(Q, pk + 32 * ic, sig + 64 * ic, side, tabs + (t >> 2) * QTAB_WORDS, q);
+    }
+    __syncthreads();
+    if (t < 64) {
+      const uint32_t* r = recs + HREC_WORDS * (t >> 3);
+      const uint32_t st = r[HREC_FLAGS] & 0xffu;
+      q_side_msm(Q, r, side, tabs + (t >> 2) * QTAB_WORDS, side ? bw + 4 * BW_TABLE : bw, q);
+      qfe x, x1;
+      q_to_cached(x, Q, q);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) x1.l[0].v[k] = __shfl_xor(x.l[0].v[k], 4, 64);   // side 1 -> side 0
+      const bool ok1 = __shfl_xor(ok ? 1 : 0, 4, 64) != 0;
+      const bool id = q_sum_is_identity(Q, x1, q);
+      const bool v = (st == HS_HALF || st == HS_DEFER) && ok && ok1 && id;
+      if (side == 0 && (t & 3) == 0 && e < cnt) verdict[ic] = v ? 1 : 0;
+    }
+    __syncthreads();   // LDS tables and records are rewritten by the next group
+  }
+}
+
+// the scalar stage of one k_chunk_half lane, out of line: inlined beside
+// curve_half the compiler interleaved the two and spilled ~580 VGPRs
+__device__ __attribute__((noinline)) uint32_t chunk_scalar_stage(uint32_t* rec, const uint8_t* pk, const uint8_t* sig,
+                                                                 const uint8_t* m, uint64_t mlen, int force_full) {
+  uint32_t dig[16];
+  const bool pre = hash_one(dig, pk, sig, m, mlen);
+  return lattice_one(rec, pre, dig, sig, force_full != 0);
+}
+
+hipError_t launch_verify_quad_list(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                                   const uint32_t* list, const unsigned long long* lcount, uint64_t max_count,
+                                   int blocks, const uint32_t* bw, uint8_t* verdict, bool force_full, hipStream_t s) {
+  if (max_count == 0) return hipSuccess;
+  const uint64_t need = (max_count + 7) / 8;
+  const uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
+  if (b == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_verify_quad_list, dim3((uint32_t)b), dim3(128), 0, s, pk, sig, blob, off, list, lcount, bw,
+                     verdict, force_full ? 1 : 0);
+  return hipGetLastError();
+}
+
+// k_chunk_half: one launch per chunk of a host-buffer call (pv_verify_batch).
+// Persistent grid over 64-signature wave tasks; a task runs the pre-checks,
+// SHA-512(R||A||M) and the lattice stage (one lane per signature, record in
+// `rec`) and then the half-size curve stage on the same lanes.  With no hash /
+// lattice launches between the chunks' curve grids, chunk c + 1's waves
+// (other stream) take the slots chunk c's waves release as they finish.
+// Deferred records (~0.2 %) are appended to `dlist` as base + i (the shard
+// index) for one k_verify_quad_list pass after the last chunk; their verdicts
+// are not written here.  No bitmap.
+__global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_chunk_half(
+    const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ blob,
+    const uint64_t* __restrict__ off, uint64_t n, uint32_t* __restrict__ rec, const uint32_t* __restrict__ bw,
+    uint32_t* __restrict__ scratch, uint8_t* __restrict__ verdict, uint32_t* __restrict__ dlist,
+    unsigned long long* __restrict__ dcount, uint64_t base, unsigned long long* __restrict__ tasks, int force_full) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint64_t gl = (uint64_t)blockIdx.x * CURVE_BLOCK + threadIdx.x;
+  uint32_t* scr = scratch + (gl / PV_HALF_LS) * (uint64_t)(HALF_LANE_WORDS * PV_HALF_LS) + gl % PV_HALF_LS;
+  const uint64_t ntask = (n + 63) / 64;
+  for (;;) {
+    const uint64_t t = wave_task(tasks);
+    if (t >= ntask) break;
+    const uint64_t i = t * 64 + lane;
+    uint32_t* r = rec + HREC_WORDS * (i < n ? i : 0);
+    uint32_t st = HS_NONE;
+    if (i < n) {
+      st = chunk_scalar_stage(r, pk + 32 * i, sig + 64 * i, blob + off[i], off[i + 1] - off[i], force_full);
+    }
+    const bool defer = st == HS_DEFER;
+    const uint64_t m = __ballot(defer);
+    if (m) {
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      unsigned long long b = 0;
+      if (lane == leader) b = atomicAdd(dcount, (unsigned long long)__popcll(m));
+      b = __shfl(b, leader, 64);
+      if (defer) dlist[b + (uint64_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(base + i);
+    }
+    bool ok = false;
+    if (st == HS_HALF) ok = curve_half<PV_HALF_LS>(pk + 32 * i, sig + 64 * i, r, scr, bw, bw + 4 * BW_TABLE);
+    if (i < n && !defer) verdict[i] = ok ? 1 : 0;
+  }
+}
+
+hipError_t launch_chunk_half(const uint8_t* pk, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                             uint64_t n, uint32_t* rec, const uint32_t* bw, uint32_t* scratch, uint64_t scratch_lanes,
+                             uint8_t* verdict, uint32_t* dlist, unsigned long long* dcount, uint64_t base,
+                             unsigned long long* tasks, int blocks, bool force_full, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (base + n > 0xffffffffull) return hipErrorInvalidValue;   // deferred indices are 32-bit
+  hipError_t e = hipMemsetAsync(tasks, 0, sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  const uint64_t need = (n + CURVE_BLOCK - 1) / CURVE_BLOCK;
+  uint64_t b = (uint64_t)blocks < need ? (uint64_t)blocks : need;
+  if (b * CURVE_BLOCK > scratch_lanes) b = scratch_lanes / CURVE_BLOCK;
+  if (b == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_chunk_half, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, blob, off, n, rec, bw, scratch,
+                     verdict, dlist, dcount, base, tasks, force_full ? 1 : 0);
+  return hipGetLastError();
+}
+
 hipError_t curve_half_occupancy(int* blocks_per_cu) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void*>(k_curve_half),
                                                       CURVE_BLOCK, 0);

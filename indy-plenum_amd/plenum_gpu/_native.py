@@ -66,6 +66,7 @@ SIGNATURES = [
     ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_set_lat_max', ctypes.c_int, [ctypes.c_uint64]),
     ('pv_set_lat_kernel', ctypes.c_int, [ctypes.c_uint32]),
+    ('pv_set_host_fused', ctypes.c_int, [ctypes.c_int]),
     ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
     ('pv_kernel_timing', ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
@@ -106,6 +107,12 @@ def set_lat_kernel(name):
     """Latency kernel on every initialised device: 'quad' (default, lane quads
     per point) or 'pair' (the lane-pair kernel, A/B) (pv_set_lat_kernel)."""
     _check('pv_set_lat_kernel', load().pv_set_lat_kernel(LAT_KERNELS[name]))
+
+
+def set_host_fused(enable):
+    """Host-buffer chunks: one fused launch per chunk + a deferred pass (True,
+    default) or the hash / lattice / curve launches per chunk (pv_set_host_fused)."""
+    _check('pv_set_host_fused', load().pv_set_host_fused(1 if enable else 0))
 
 
 STAGING_MODES = {0: 'pinned', 1: 'pageable'}   # PV_STAGING_PINNED / _PAGEABLE

@@ -182,9 +182,9 @@ def test_host_pipeline_multi_chunk(nat, shape):
     blob = b.blob.cpu().numpy()[:int(off[-1])]
     want = ~b.tamper.cpu().numpy().astype(bool)
     # pinned staging ring with threaded and single-thread gathers (4 chunks:
-    # 32768 + 2 x 83616 signatures; 16 chunks: 32768 + 5 x ~33446, so chunks
-    # 2.. wait for their slot's previous DMA and reuse a workspace; the tail
-    # case below: 32768 + 3 x ~32769), one chunk, and the runtime's pageable
+    # a 32768 ramp chunk + 4 x ~41808 signatures; 16 chunks: 6 x ~33333, so
+    # chunks 2.. wait for their slot's previous DMA and reuse a workspace; the
+    # tail case below: 4 x ~32769), one chunk, and the runtime's pageable
     # staging
     try:
         for staging, threads, chunks in (('pinned', 8, 4), ('pinned', 1, 1), ('pageable', 0, 4), ('pinned', 8, 16)):
@@ -197,6 +197,47 @@ def test_host_pipeline_multi_chunk(nat, shape):
             assert (got == want[:131075]).all(), (shape, staging, threads)
     finally:
         nat.set_host_staging('pinned', 8, 8)
+
+
+def test_host_fused_chunks_and_deferred_pass(nat, raw_vectors, adversarial):
+    """Host-buffer chunks run one fused launch each (k_chunk_half: hash +
+    lattice + half-size curve per task) and the deferred records one
+    lane-quad pass over a device-side index list: same verdicts as the
+    per-chunk hash / lattice / curve schedule on a 200k C2 batch (~400
+    deferred, several chunks); with PV_CURVE_MODE=full every record is listed,
+    so the list pass loops over 200k entries with its fixed grid; the
+    fixtures (mixed-order, non-canonical, small-order cases) through the
+    chunk path (latency path off) match libsodium in both modes."""
+    from plenum_gpu.device import SyntheticBatch
+    from plenum_gpu.nacl_wrappers import verify_signed_batch
+    from conftest import split_sm
+    b = SyntheticBatch(0, 200000, 256, cfg=2, first=5151)
+    off = b.off.cpu().numpy().astype(np.uint64)
+    pk, sig, blob = b.pk.cpu().numpy(), b.sig.cpu().numpy(), b.blob.cpu().numpy()[:int(off[-1])]
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    rows = split_sm(adversarial)
+    r = raw_vectors
+    try:
+        nat.set_host_staging('pinned', 8, 8)
+        for fused in (True, False):
+            nat.set_host_fused(fused)
+            got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=False)
+            assert (got == want).all(), (fused, int((got != want).sum()))
+        nat.set_host_fused(True)
+        nat.set_lat_max(0)
+        for mode in ('half', 'full'):
+            nat.set_curve_mode(mode)
+            got = nat.verify_batch_arrays(pk, sig, blob, off, dedup_keys=False)
+            assert (got == want).all(), (mode, int((got != want).sum()))
+            got = nat.verify_batch_arrays(r['pk'], r['sig'], r['blob'], r['off'])
+            assert (got == r['verdict'].astype(bool)).all(), mode
+            got = verify_signed_batch([(p, sm) for _, p, sm, _ in rows])
+            wrong = [rows[k][0] for k in range(len(rows)) if got[k] != rows[k][3]]
+            assert not wrong, (mode, wrong)
+    finally:
+        nat.set_host_fused(True)
+        nat.set_curve_mode('half')
+        nat.set_lat_max(nat.LAT_MAX_DEFAULT)
 
 
 def test_host_page_locked_inputs_direct(nat):

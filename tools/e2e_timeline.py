@@ -2,8 +2,8 @@
 --kernel-trace csv directory (tools/e2e_trace.py under rocprofv3).  Copies are
 not used: rocprofiler-sdk drops async-copy completion callbacks on this image
 (it times out waiting for them), so a copy timeline is incomplete.  The last
-call = from the k_hash launch of its first chunk (the last `chunks` curve
-launches).  Prints the events, the GPU kernel-busy union and the kernel
+call = from the k_hash launch (or the fused k_chunk_half launch) of its first
+chunk (the last `chunks` per-chunk grids).  Prints the events, the GPU kernel-busy union and the kernel
 overlap between consecutive chunks (two compute streams).
     python tools/e2e_timeline.py DIR [chunks]"""
 import csv
@@ -18,9 +18,13 @@ def main(d, chunks=9):
         for r in csv.DictReader(open(fn)):
             ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0]))
     ev.sort()
-    curves = [i for i, e in enumerate(ev) if 'k_curve' in e[2]]
+    # per-chunk grids: k_curve_half (hash / lattice / curve schedule) or
+    # k_chunk_half (fused chunks, PV_HOST_FUSED=1; no k_hash before them)
+    curves = [i for i, e in enumerate(ev) if 'k_curve' in e[2] or 'k_chunk_half' in e[2]]
     first_curve = curves[-chunks]
-    start = max(i for i in range(first_curve) if 'k_hash' in ev[i][2])
+    prev = curves[-chunks - 1] if len(curves) > chunks else -1
+    hashes = [i for i in range(prev + 1, first_curve) if 'k_hash' in ev[i][2]]
+    start = max(hashes) if hashes else first_curve
     last = ev[start:]
     t0 = last[0][0]
     print('# last call: {} chunks; start end dur (us) kernel'.format(chunks))
