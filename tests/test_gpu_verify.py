@@ -49,7 +49,21 @@ def test_empty_and_single(nat, raw_vectors):
         assert got[0] == bool(r['verdict'][i])
 
 
-def test_random_ragged_vs_oracle(nat):
+@pytest.mark.parametrize('path', ['default', 'chunks'])
+def test_random_ragged_vs_oracle(nat, path):
+    """Ragged messages (0 B - 5 KB) with ~10 % corrupted, against the oracle:
+    through the latency kernel (default size routing) and through the fused
+    chunk path (latency path off: per-lane SHA-512 of ragged lengths inside
+    k_chunk_half, deferred records in the list pass)."""
+    if path == 'chunks':
+        nat.set_lat_max(0)
+    try:
+        _random_ragged_vs_oracle(nat)
+    finally:
+        nat.set_lat_max(nat.LAT_MAX_DEFAULT)
+
+
+def _random_ragged_vs_oracle(nat):
     rng = np.random.default_rng(2026)
     n = 6000
     seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
