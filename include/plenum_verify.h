@@ -301,8 +301,10 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
 
 /* Host-side staging of pv_verify_batch's inputs, chosen by PV_HOST_STAGING /
  * PV_HOST_COPY_THREADS / PV_HOST_CHUNKS at pv_init.  A shard runs as a
- * pipeline of chunks: a short first chunk (half a regular one) so the kernels
- * start early, then about `chunks` equal chunks of >= 32768 signatures.
+ * pipeline of chunks: short leading chunks (32768, 65536, ... signatures below
+ * a regular chunk; PV_HOST_RAMP env, 0 = one first chunk of PV_HOST_FIRST_PCT %
+ * of a regular one) so the kernels start early, then about `chunks` equal
+ * chunks of >= 32768 signatures.
  *   PV_STAGING_PINNED   ("pinned", default) each chunk is gathered by up to
  *                       copy_threads host threads into one of two page-locked
  *                       slots per device and DMA'd from there; verdicts come
