@@ -1,6 +1,7 @@
 #!/bin/bash
 # Fused host chunks over 2 vs 3 compute streams, with ramps starting at 8k /
 # 16k / 32k signatures (C2 end_to_end, interleaved).  bash tools/gpu_fused_streams.sh OUT
+# (PV_HOST_STREAMS was removed after this A/B: profiles/r02_ab_fused_streams_notadopted.jsonl)
 set -u
 out=${1:-gpurun_out/fstreams}
 mkdir -p "$out"
