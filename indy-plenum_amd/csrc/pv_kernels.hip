@@ -829,7 +829,12 @@ hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32
 }
 
 // -------------------------------------------------------------- key cache
-__global__ __launch_bounds__(256, 2) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
+// waves per SIMD k_keys is compiled for: 3 (168 VGPRs, 248 B of spills) measured
+// 1 % slower on C4 than 2 (profiles/r02_ab_keys_waves_notadopted.jsonl)
+#ifndef PV_KEYS_WAVES
+#define PV_KEYS_WAVES 2
+#endif
+__global__ __launch_bounds__(256, PV_KEYS_WAVES) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
                                                uint32_t* __restrict__ scr) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j < k) key_prepare(ktab + j * KEY_WORDS, scr + j * KEY_SCRATCH, pk + 32 * j);
