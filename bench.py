@@ -313,11 +313,11 @@ def main_c1(args):
         authnr.addIdr(idr, vk)
     want = [[idr] for idr, _ in ids]
     for _ in range(args.warmup):
-        authnr.authenticate_batch(reqs)
+        authnr.authenticate_batch(reqs, pause_gc=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = authnr.authenticate_batch(reqs)
+        out = authnr.authenticate_batch(reqs, pause_gc=True)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     mism = sum(1 for a, b in zip(out, want) if a != b)

@@ -296,14 +296,36 @@ struct Workspace {
   DevBuf<uint32_t> hrec, dlist;        // lattice records, deferred indices (half-size path)
   DevBuf<unsigned long long> qc;       // [0] deferred count, [1] curve task queue
   bool half_ran = false;               // qc[0] holds the last generic batch's deferred count
+  // last use: recorded after every enqueue on this workspace (whatever stream
+  // it ran on); the next use on another stream waits for it, so an async batch
+  // still running on a caller's stream never shares scratch / h / hrec / qc /
+  // counter / bitmap with a later sync, host-buffer or async call
+  hipEvent_t done = nullptr;
+  hipStream_t done_on = nullptr;
   void release() {
     scratch.release(); h.release(); counter.release(); pre.release(); bitmap.release();
     hrec.release(); dlist.release(); qc.release();
+    if (done) (void)hipEventDestroy(done);
+    done = nullptr;
+    done_on = nullptr;
   }
 };
 
+// order a use of workspace w on stream s after its previous use
+int ws_begin(Workspace& w, hipStream_t s) {
+  if (w.done_on && w.done_on != s) HIP_OK(hipStreamWaitEvent(s, w.done, 0));
+  return PV_OK;
+}
+
+int ws_end(Workspace& w, hipStream_t s) {
+  HIP_OK(hipEventRecord(w.done, s));
+  w.done_on = s;
+  return PV_OK;
+}
+
 struct Device {
-  int id = -1;
+  int id = -1;   // engine device id: the device_mask bit and the `device` argument
+  int ord = -1;  // HIP ordinal (== id, except under PV_TEST_DUP_DEVICE)
   hipStream_t stream = nullptr;
   hipStream_t copy = nullptr;   // host-buffer calls: H2D of chunk c+1 overlaps the kernels of chunk c
   hipEvent_t copied = nullptr;  // recorded on `copy` after each chunk's inputs, waited on by `stream`
@@ -390,7 +412,7 @@ Device* find_dev(int id) {
 }
 
 int init_device(Device& d) {
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   d.ws[0].stream = d.stream;
   HIP_OK(hipStreamCreateWithFlags(&d.ws[1].stream, hipStreamNonBlocking));
@@ -399,6 +421,7 @@ int init_device(Device& d) {
   for (auto& e : d.staged) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&d.keys_ready, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&d.joined, hipEventDisableTiming));
+  for (auto& w : d.ws) HIP_OK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
   if (const char* m = getenv("PV_HOST_STAGING")) {
     if (!strcmp(m, "pageable")) d.pinned = false;
     else if (strcmp(m, "pinned") != 0) return fail(PV_EINVAL, "PV_HOST_STAGING must be pinned or pageable (got %s)", m);
@@ -441,7 +464,7 @@ int init_device(Device& d) {
       return fail(PV_EINVAL, "PV_HOST_COPY_THREADS must be in 1..64 (got %s)", t);
   }
   hipDeviceProp_t prop;
-  HIP_OK(hipGetDeviceProperties(&prop, d.id));
+  HIP_OK(hipGetDeviceProperties(&prop, d.ord));
   d.cu_count = prop.multiProcessorCount;
   HIP_OK(d.btab.ensure(pv::BTAB_CHUNKS * pv::BTAB_ENTRIES * pv::BTAB_WORDS));
   HIP_OK(pv::launch_btable_init(d.btab.p, d.stream));
@@ -491,7 +514,7 @@ int init_device(Device& d) {
 
 void release_device(Device& d) {
   if (d.id < 0) return;
-  (void)hipSetDevice(d.id);
+  (void)hipSetDevice(d.ord);
   for (auto& w : d.ws)
     if (w.stream) (void)hipStreamSynchronize(w.stream);
   d.btab.release(); d.bw.release(); d.counter.release();
@@ -640,7 +663,8 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
     lev = d.live_pool[d.live_used++].e;
     ++d.live_launches;
   }
-  int rc = PV_OK;
+  int rc = ws_begin(w, s);
+  if (rc) return rc;
   uint64_t* bm = stage_bitmap(w, bitmap, n, rc);
   if (rc) return rc;
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
@@ -651,6 +675,8 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (lev) HIP_OK(hipEventRecord(lev[1], s));
   rc = enqueue_curve(d, w, pk, sig, blob, off, n, verdict, bm, s, ktab, kidx);
+  if (rc) return rc;
+  rc = ws_end(w, s);
   if (rc) return rc;
   if (lev) HIP_OK(hipEventRecord(lev[2], s));
   if (timed) {
@@ -720,12 +746,12 @@ uint64_t small_bytes(const HostBatch& hb, uint64_t s, uint64_t e) {
 
 int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   const uint64_t m = e - s;
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   Workspace& w = d.ws[0];
   struct Drain {
     Device& d;
     ~Drain() {
-      (void)hipSetDevice(d.id);
+      (void)hipSetDevice(d.ord);
       (void)hipStreamSynchronize(d.ws[0].stream);
     }
   } drain{d};
@@ -759,6 +785,10 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
 }
 
 int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
+  // before any size arithmetic: a shard whose end offset lies below its start
+  // would wrap bytes + 16 (the per-chunk checks come later)
+  if (hb.off[e] < hb.off[s])
+    return fail(PV_EINVAL, "msg_off not monotone in [%llu, %llu]", (unsigned long long)s, (unsigned long long)e);
   const uint64_t m = e - s;
   if (m == 0) return PV_OK;
   if (m <= d.lat_max && d.lat_quad && d.mode != CurveMode::Grouped && d.pinned &&
@@ -766,16 +796,21 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     const int rc = run_small(d, hb, s, e);
     if (rc != 1) return rc;
   }
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   // on every exit (errors included) wait for the work that reads host memory
   struct Drain {
     Device& d;
     ~Drain() {
-      (void)hipSetDevice(d.id);
+      (void)hipSetDevice(d.ord);
       (void)hipStreamSynchronize(d.copy);
       for (auto& w : d.ws) (void)hipStreamSynchronize(w.stream);
     }
   } drain{d};
+  // async batches may still hold either workspace on a caller's stream
+  for (auto& w : d.ws) {
+    const int rc = ws_begin(w, w.stream);
+    if (rc) return rc;
+  }
   const uint8_t* pk = hb.pk;
   const uint64_t b0 = hb.off[s], bytes = hb.off[e] - b0;
   // PV_FLAG_DEDUP_KEYS: prepare each distinct key once (cached multiples of
@@ -856,6 +891,12 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     if (!d.pinned || cap <= d.pin_max || reg == PV_HOST_CHUNK_MIN || hc >= 4096) break;
   }
   const size_t nch = bounds.size() - 1;
+  // chunk sizes come from the offsets at the chunk bounds: check those before
+  // anything is sized from them (each chunk's offsets are checked as they are copied)
+  for (size_t j = 1; j < bounds.size(); ++j)
+    if (hb.off[s + bounds[j]] < hb.off[s + bounds[j - 1]])
+      return fail(PV_EINVAL, "msg_off not monotone in [%llu, %llu]", (unsigned long long)(s + bounds[j - 1]),
+                  (unsigned long long)(s + bounds[j]));
   bool pinned = d.pinned && cap <= d.pin_max;
   if (pinned && (d.pin[0].ensure(cap) != hipSuccess || d.pin[1].ensure(cap) != hipSuccess ||
                  d.vout.ensure(m) != hipSuccess)) {
@@ -961,6 +1002,7 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
       HIP_OK(pv::launch_chunk_half(d.pk.p + 32 * c0, d.sig.p + 64 * c0, d.blob.p, d.off.p + c0, mc, w.hrec.p, d.bw.p,
                                    w.scratch.p, w.scratch.cap / pv::HALF_SCRATCH_WORDS, d.verdict.p + c0, d.dl.p,
                                    d.dlc.p, c0, w.qc.p + 1, d.curve_half_blocks, d.mode == CurveMode::Full, w.stream));
+      if (const int rc = ws_end(w, w.stream)) return rc;
       if (trace)
         fprintf(stderr, "[pv host] chunk %zu (%llu sigs): begin %.1f slot-free %.1f gathered %.1f enqueued %.1f us\n", c,
                 (unsigned long long)mc, t_begin, t_slot, t_gather, us());
@@ -1010,11 +1052,22 @@ int pv_init(uint32_t device_mask) {
   int count = 0;
   hipError_t e = hipGetDeviceCount(&count);
   if (e != hipSuccess || count <= 0) return fail(PV_ENODEV, "no HIP device available (%s)", hipGetErrorString(e));
-  for (int id = 0; id < count && id < 32; ++id) {
+  // PV_TEST_DUP_DEVICE=k (test only, 2..8): k engine devices 0..k-1 all on HIP
+  // device 0, so the multi-device paths (one worker thread per device, shard
+  // offsets, error aggregation) run on a one-GPU box
+  int dup = 0;
+  if (const char* t = getenv("PV_TEST_DUP_DEVICE")) {
+    dup = atoi(t);
+    if (dup == 1) dup = 2;
+    if (dup < 0 || dup > 8) return fail(PV_EINVAL, "PV_TEST_DUP_DEVICE must be in 0..8 (got %s)", t);
+  }
+  const int n_ids = dup ? dup : count;
+  for (int id = 0; id < n_ids && id < 32; ++id) {
     if (device_mask && !((device_mask >> id) & 1u)) continue;
     if (find_dev(id)) continue;
     g_devs.emplace_back();
     g_devs.back().id = id;
+    g_devs.back().ord = dup ? 0 : id;
     int rc = init_device(g_devs.back());
     if (rc != PV_OK) {
       release_device(g_devs.back());
@@ -1056,6 +1109,12 @@ int pv_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_bl
   const HostBatch hb{pk, sig, msg_blob, msg_off, verdict, flags};
   const uint64_t G = devs.size();
   if (G == 1) return run_shard(*devs[0], hb, 0, n);
+  // O(G) pre-check of the shard boundaries (each shard also checks its own
+  // range first, and every chunk its offsets while they are copied)
+  for (uint64_t g = 0; g < G; ++g)
+    if (msg_off[n * (g + 1) / G] < msg_off[n * g / G])
+      return fail(PV_EINVAL, "msg_off not monotone in shard %llu [%llu, %llu]", (unsigned long long)g,
+                  (unsigned long long)(n * g / G), (unsigned long long)(n * (g + 1) / G));
   // one worker thread per device: each gathers, stages and launches its own
   // shard, so no device waits on another's host gathers (errors come back as
   // codes + messages; no exception crosses the ABI)
@@ -1094,7 +1153,7 @@ int pv_verify_batch_device(const uint8_t* pk, const uint8_t* sig, const uint8_t*
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (n == 0) return PV_OK;
   if (!pk || !sig || !msg_blob || !msg_off || !verdict) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   int rc = enqueue_verify(*d, d->ws[0], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr);
   if (rc) return rc;
@@ -1112,7 +1171,7 @@ int pv_verify_batch_device_async(const uint8_t* pk, const uint8_t* sig, const ui
   if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
   if (n == 0) return PV_OK;
   if (!pk || !sig || !msg_blob || !msg_off || !verdict || !bitmap) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
   return enqueue_verify(*d, d->ws[slot], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr);
 }
@@ -1128,7 +1187,7 @@ int pv_verify_keyed_device_async(const uint32_t* ktab, const uint32_t* key_idx, 
   if (n == 0) return PV_OK;
   if (!ktab || !key_idx || !pk || !sig || !msg_blob || !msg_off || !verdict || !bitmap)
     return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
   return enqueue_verify(*d, d->ws[slot], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr,
                         ktab, key_idx);
@@ -1142,12 +1201,16 @@ int pv_keys_prepare_device_async(const uint8_t* pk, uint64_t k, uint32_t* ktab, 
   if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
   if (k == 0) return PV_OK;
   if (!pk || !ktab) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
+  // the key scratch of slot i is ordered like workspace i (the host pipeline
+  // prepares keys in kscr on ws[0]'s stream)
+  int rc = ws_begin(d->ws[slot], s);
+  if (rc) return rc;
   DevBuf<uint32_t>& scr = slot ? d->kscr2 : d->kscr;
   HIP_OK(scr.ensure(k * pv::KEYTAB_SCRATCH));
   HIP_OK(pv::launch_keys(pk, k, ktab, scr.p, s));
-  return PV_OK;
+  return ws_end(d->ws[slot], s);
 }
 
 int pv_keys_prepare_device(const uint8_t* pk, uint64_t k, uint32_t* ktab, int device, void* stream) {
@@ -1157,10 +1220,14 @@ int pv_keys_prepare_device(const uint8_t* pk, uint64_t k, uint32_t* ktab, int de
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (k == 0) return PV_OK;
   if (!pk || !ktab) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  int rc = ws_begin(d->ws[0], s);
+  if (rc) return rc;
   HIP_OK(d->kscr.ensure(k * pv::KEYTAB_SCRATCH));
   HIP_OK(pv::launch_keys(pk, k, ktab, d->kscr.p, s));
+  rc = ws_end(d->ws[0], s);
+  if (rc) return rc;
   HIP_OK(hipStreamSynchronize(s));
   return PV_OK;
 }
@@ -1174,7 +1241,7 @@ int pv_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const 
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (n == 0) return PV_OK;
   if (!ktab || !key_idx || !pk || !sig || !msg_blob || !msg_off || !verdict) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   int rc = enqueue_verify(*d, d->ws[0], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr, ktab,
                           key_idx);
@@ -1192,7 +1259,7 @@ int pv_time_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, c
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (iters <= 0) return fail(PV_EINVAL, "iters must be > 0");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   float a = 0, b = 0;
   for (int it = 0; it < iters; ++it) {
@@ -1212,7 +1279,7 @@ int pv_time_verify_device(const uint8_t* pk, const uint8_t* sig, const uint8_t* 
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (iters <= 0) return fail(PV_EINVAL, "iters must be > 0");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   float a = 0, b = 0;
   for (int it = 0; it < iters; ++it) {
@@ -1229,7 +1296,7 @@ int pv_kernel_timing(int device, int enable, float* hash_ms, float* curve_ms, ui
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   DeviceGuard dg;
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   {
     const int rc = resolve_live(*d);
     if (rc) return rc;
@@ -1291,7 +1358,7 @@ int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks) {
     if (copy_threads) d.copy_threads = copy_threads;
     if (chunks) d.host_chunks = chunks;
     if (!d.pinned) {  // pageable staging holds no page-locked memory
-      (void)hipSetDevice(d.id);
+      (void)hipSetDevice(d.ord);
       (void)hipStreamSynchronize(d.copy);
       d.pin[0].release();
       d.pin[1].release();
@@ -1312,8 +1379,8 @@ int pv_curve_stats(int device, uint32_t* mode, uint64_t* deferred) {
     *deferred = 0;
     Workspace& w = d->ws[d->last_ws];
     if (w.half_ran) {
-      HIP_OK(hipSetDevice(device));
-      HIP_OK(hipStreamSynchronize(w.stream));
+      HIP_OK(hipSetDevice(d->ord));
+      HIP_OK(w.done_on ? hipEventSynchronize(w.done) : hipStreamSynchronize(w.stream));
       HIP_OK(hipMemcpy(deferred, w.qc.p, sizeof(uint64_t), hipMemcpyDeviceToHost));
     }
   }
@@ -1330,7 +1397,7 @@ int pv_tally_votes_device(const uint8_t* verdict, const uint32_t* sender, const 
   if (n_nodes == 0 || n_nodes > 1024) return fail(PV_EINVAL, "n_nodes must be in 1..1024");
   if (n_batches == 0) return PV_OK;
   if (!verdict || !sender || !batch_off || !votes || !reached) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   HIP_OK(d->tflag.ensure(1));
   HIP_OK(hipMemsetAsync(d->tflag.p, 0, 4, s));
@@ -1351,7 +1418,7 @@ int pv_tally_votes(const uint8_t* verdict, const uint32_t* sender, const uint64_
   if (n_batches == 0) return PV_OK;
   if (!verdict || !sender || !batch_off || !votes || !reached) return fail(PV_EINVAL, "null buffer");
   Device& d = g_devs[0];
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   const uint64_t b0 = batch_off[0], m = batch_off[n_batches] - b0;
   std::vector<uint64_t> offs(n_batches + 1);
   for (uint64_t k = 0; k <= n_batches; ++k) {
@@ -1390,7 +1457,7 @@ int pv_tally_device(const uint32_t* verdict_bits, const uint32_t* dup_mask, uint
   if (n_nodes == 0) return fail(PV_EINVAL, "n_nodes must be >= 1");
   if (n_batches == 0) return PV_OK;
   if (!verdict_bits || !reached) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   HIP_OK(pv::launch_tally_bits(verdict_bits, dup_mask, n_batches, n_nodes, quorum, votes, reached, s));
   HIP_OK(hipStreamSynchronize(s));
@@ -1406,7 +1473,7 @@ int pv_tally(const uint32_t* verdict_bits, const uint32_t* dup_mask, uint64_t n_
   if (n_batches == 0) return PV_OK;
   if (!verdict_bits || !reached) return fail(PV_EINVAL, "null buffer");
   Device& d = g_devs[0];
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   const uint64_t words = n_batches * ((n_nodes + 31) / 32);
   HIP_OK(d.tbits.ensure(2 * words));
   HIP_OK(d.reached.ensure(n_batches));
@@ -1426,7 +1493,7 @@ int pv_sign_batch_device(const uint8_t* seeds, const uint8_t* msg_blob, const ui
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (n == 0) return PV_OK;
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   HIP_OK(pv::launch_sign(seeds, msg_blob, msg_off, n, d->btab.p, pk_out, sig_out, s));
   HIP_OK(hipStreamSynchronize(s));
@@ -1441,7 +1508,7 @@ int pv_sign_batch(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t*
   if (n == 0) return PV_OK;
   if (!seeds || !msg_off || !pk_out || !sig_out) return fail(PV_EINVAL, "null buffer");
   Device& d = g_devs[0];
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   const uint64_t b0 = msg_off[0], bytes = msg_off[n] - b0;
   std::vector<uint64_t> offs(n + 1);
   for (uint64_t k = 0; k <= n; ++k) offs[k] = msg_off[k] - b0;
@@ -1500,7 +1567,7 @@ int pv_sha256_batch_device(const uint8_t* blob, const uint64_t* off, uint64_t n,
   if (n == 0) return PV_OK;
   if (!blob || !off || !digests) return fail(PV_EINVAL, "null device buffer");
   if (prefix > 255) return fail(PV_EINVAL, "prefix must be -1 (none) or a byte value");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   HIP_OK(pv::launch_sha256(blob, off, n, prefix < 0 ? 0 : 1, prefix < 0 ? 0 : (uint32_t)prefix, d->counter.p,
                            reinterpret_cast<uint32_t*>(digests), d->sha256_blocks, s));
@@ -1515,7 +1582,7 @@ int pv_merkle_root_device(const uint8_t* blob, const uint64_t* off, uint64_t n, 
   Device* d = find_dev(device);
   if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
   if (!root || (n && (!blob || !off))) return fail(PV_EINVAL, "null device buffer");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   uint32_t* leaves = reinterpret_cast<uint32_t*>(leaf_hashes);
   if (!leaves && n) {
@@ -1538,7 +1605,7 @@ int pv_merkle_root(const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t
   for (uint64_t i = 0; i < n; ++i)
     if (off[i + 1] < off[i]) return fail(PV_EINVAL, "off not monotone at %llu", (unsigned long long)i);
   Device& d = g_devs[0];
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   const uint64_t b0 = n ? off[0] : 0, bytes = n ? off[n] - b0 : 0;
   std::vector<uint64_t> offs(n + 1);
   for (uint64_t k = 0; k <= n; ++k) offs[k] = n ? off[k] - b0 : 0;
@@ -1569,7 +1636,7 @@ int pv_sha256_batch(const uint8_t* blob, const uint64_t* off, uint64_t n, int32_
   for (uint64_t i = 0; i < n; ++i)
     if (off[i + 1] < off[i]) return fail(PV_EINVAL, "off not monotone at %llu", (unsigned long long)i);
   Device& d = g_devs[0];
-  HIP_OK(hipSetDevice(d.id));
+  HIP_OK(hipSetDevice(d.ord));
   const uint64_t b0 = off[0], bytes = off[n] - b0;
   std::vector<uint64_t> offs(n + 1);
   for (uint64_t k = 0; k <= n; ++k) offs[k] = off[k] - b0;
@@ -1597,7 +1664,7 @@ int pv_synth_layout_device(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t
   if (mode == PV_SYNTH_RANGE && mlen_max < mlen_min) return fail(PV_EINVAL, "mlen_max < mlen_min");
   if (mode == PV_SYNTH_COMMIT && (n_nodes == 0 || n_nodes > 1024))
     return fail(PV_EINVAL, "n_nodes must be in 1..1024");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   HIP_OK(d->scan.ensure(pv::scan_sums_words(n + 1)));
   HIP_OK(pv::launch_synth_layout(cfg, mode, first, n, mlen_min, mlen_max, n_nodes, off, d->scan.p, s));
@@ -1616,7 +1683,7 @@ int pv_synth_fill_device(uint32_t cfg, uint32_t mode, uint64_t first, uint64_t n
   if (mode > PV_SYNTH_COMMIT) return fail(PV_EINVAL, "unknown synth mode %u", mode);
   if (mode == PV_SYNTH_COMMIT && (n_nodes == 0 || n_nodes > 1024))
     return fail(PV_EINVAL, "n_nodes must be in 1..1024");
-  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipSetDevice(d->ord));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   uint64_t total = 0;
   HIP_OK(hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, s));

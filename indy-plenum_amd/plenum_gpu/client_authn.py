@@ -346,20 +346,26 @@ class CoreAuthMixin:
         t = type(self)
         return t.authenticate is CoreAuthMixin.authenticate and t.authenticate_multi is NaclAuthNr.authenticate_multi
 
-    def authenticate_batch(self, reqs, threshold: Optional[int] = None, verifier: Verifier = DidVerifier):
+    def authenticate_batch(self, reqs, threshold: Optional[int] = None, verifier: Verifier = DidVerifier,
+                           pause_gc: bool = False):
         """[identifiers list | SigningException/other exception] per request.
         One GPU pass for the batch, then the reference's per-request control
         flow; the replay reuses the prefetch's signing view, decoded signature,
         serialized message and key object of each request (computed from the
-        same objects by the same pure functions within this call)."""
-        # the batch allocates a few container objects per request and keeps
-        # them until the replay: with the cyclic collector running, that
-        # triggers full collections over the whole heap (C1 on the GPU box:
-        # median 123 ms vs 49 ms per 10k requests, tools/ab_c1_replay.py), so
-        # it is paused for the call and restored after (nothing here makes
-        # cycles; the garbage is reclaimed by reference counting)
-        gc_was_on = gc.isenabled()
-        gc.disable()
+        same objects by the same pure functions within this call).
+
+        pause_gc (opt-in): the batch allocates a few container objects per
+        request and keeps them until the replay; with the cyclic collector
+        running that triggers full collections over the whole heap (C1 on the
+        GPU box: median 123 ms vs 49 ms per 10k requests,
+        tools/ab_c1_replay.py).  pause_gc=True disables the collector for the
+        call -- process-wide, so other threads' collections wait too -- and
+        restores it after.  Rejected requests do create reference cycles
+        (exception -> traceback -> frame -> `out` -> exception); those are
+        reclaimed by the first collection after the call."""
+        gc_was_on = pause_gc and gc.isenabled()
+        if gc_was_on:
+            gc.disable()
         try:
             views = {} if self._replay_reuses_prefetch() else None
             self.verify_batch(reqs, verifier, _views=views)

@@ -29,7 +29,7 @@ def main():
         for mode in res:
             CoreAuthMixin._replay_reuses_prefetch = stock if mode != 'plain' else (lambda self: False)
             t0 = time.perf_counter()
-            out = a.authenticate_batch(reqs)
+            out = a.authenticate_batch(reqs, pause_gc=True)
             res[mode].append(time.perf_counter() - t0)
             assert out == want and gc.isenabled()
     CoreAuthMixin._replay_reuses_prefetch = stock
