@@ -321,6 +321,75 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
 #define PV_STAGING_PAGEABLE 1u
 int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks);
 
+
+/* ------------------------------------------------------------------------
+ * BLS COMMIT check
+ *
+ *   pv_bls_verify_batch  replaces n calls of
+ *                        BlsCryptoVerifierIndyCrypto.verify_sig(signature, message, bls_pk)
+ *                        (crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:73-82), made by
+ *                        BlsBftReplicaPlenum._validate_signature for every COMMIT
+ *                        (plenum/bls/bls_bft_replica_plenum.py:55-75, 194-213), i.e.
+ *                        python-ursa 0.1.1 Bls.verify(sig, msg, vk, gen):
+ *                        e(sigma, g) == e(H(msg), vk) over Milagro AMCL BN254.
+ *   pv_bls_set_keys      the fixed G2 arguments of those checks: the group generator
+ *                        (BlsGroupParamsLoaderIndyCrypto, bls_crypto_indy_crypto.py:15-20)
+ *                        and the nodes' keys (bls_key_register.get_key_by_name);
+ *                        replaces IndyCryptoBlsUtils.bls_from_str(v, VerKey) (:38-52)
+ *                        + the pairing's G2 precomputation.
+ *   pv_bls_sign_batch[_device], pv_bls_pubkeys
+ *                        batch counterparts of Bls.sign / VerKey.new (data generation).
+ *
+ * PARITY UNPINNED: ursa / AMCL are not in the reference and not installed; the
+ * reference holds no BLS vector.  Encodings (128-byte representations):
+ *   sigma  0x04|x|y (uncompressed) or 0x02/0x03|x (compressed), big-endian, rest
+ *          ignored; x or y >= p, another prefix, or a point off y^2 = x^3 + 2 is
+ *          the point at infinity O (AMCL ECP::frombytes).  A representation that
+ *          is not 128 bytes fails to decode: verdict 0 (sig_len).
+ *   keys   x.a|x.b|y.a|y.b, big-endian, each taken mod p (ECP2::frombytes);
+ *          off the twist y^2 = x^3 + 2/(1+i) = O.
+ *   H(m)   SHA-256(m) as a big-endian integer mod p, try-and-increment on x,
+ *          y = (x^3+2)^((p+1)/4) (ursa PointG1::from_hash / AMCL ECP::new_big).
+ *   e(O, .) = e(., O) = 1: sigma = O or key = O verify iff both are O.
+ * Errors of these entry points are reported by pv_bls_last_error().
+ * ---------------------------------------------------------------------- */
+#define PV_BLS_KEY_OK 0u          /* a point of order r on the twist */
+#define PV_BLS_KEY_INFINITY 1u    /* off the twist: decodes to O */
+#define PV_BLS_KEY_NOT_IN_G2 2u   /* on the twist outside the order-r subgroup: verdicts are 0 */
+
+/* Prepare the generator (128 B) and k keys (k x 128 B) on HIP device `device`:
+ * decode, subgroup check, the 70 optimal-ate lines of each point (kept on the
+ * device; replaces the previous key set).  status (k bytes, may be NULL) gets
+ * PV_BLS_KEY_*.  PV_EINVAL if the generator is not PV_BLS_KEY_OK. */
+int pv_bls_set_keys(const uint8_t *gen, const uint8_t *pks, uint64_t k, uint8_t *status, int device);
+
+/* n checks from HOST memory: check j = (sig[j] 128 B, message msg_idx[j] of
+ * msg_blob/msg_off (n_msgs messages, msg_off has n_msgs+1 entries), key
+ * key_idx[j] of the current key set) -> verdict[j] (1 = Bls.verify true).
+ * sig_len (may be NULL): the decoded representation lengths; != 128 -> 0.
+ * Every message is hashed once; checks are grouped by key on the device. */
+int pv_bls_verify_batch(const uint8_t *sig, const uint64_t *sig_len, const uint8_t *msg_blob, const uint64_t *msg_off,
+                        uint64_t n_msgs, const uint32_t *msg_idx, const uint32_t *key_idx, uint64_t n,
+                        uint8_t *verdict, int device);
+/* Same with DEVICE pointers (msg_blob needs >= 16 readable bytes past the last
+ * message); synchronous on `stream` (NULL = library stream). */
+int pv_bls_verify_batch_device(const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n_msgs,
+                               const uint32_t *msg_idx, const uint32_t *key_idx, uint64_t n, uint8_t *verdict,
+                               int device, void *stream);
+/* sig[j] = sk[key_idx[j]] * H(message msg_idx[j]) (uncompressed 128 B); sks: k x 32 B big-endian */
+int pv_bls_sign_batch(const uint8_t *sks, uint64_t k, const uint8_t *msg_blob, const uint64_t *msg_off,
+                      uint64_t n_msgs, const uint32_t *msg_idx, const uint32_t *key_idx, uint64_t n, uint8_t *sig,
+                      int device);
+int pv_bls_sign_batch_device(const uint8_t *sks, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n_msgs,
+                             const uint32_t *msg_idx, const uint32_t *key_idx, uint64_t n, uint8_t *sig, int device,
+                             void *stream);
+/* pks[i] = sks[i] * gen (k keys, 128 B each) */
+int pv_bls_pubkeys(const uint8_t *gen, const uint8_t *sks, uint64_t k, uint8_t *pks, int device);
+/* HIP-event durations of the last verify call on `device`: message hashing and the check kernel */
+int pv_bls_kernel_ms(int device, float *hash_ms, float *verify_ms);
+const char *pv_bls_last_error(void);
+void pv_bls_shutdown(void);
+
 #ifdef __cplusplus
 }
 #endif

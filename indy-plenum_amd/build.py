@@ -21,7 +21,7 @@ LIBDIR = os.path.join(HERE, 'lib')
 LIB = os.path.join(LIBDIR, 'libplenum_verify.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
-SOURCES = ['pv_kernels.hip', 'pv_api.cpp']
+SOURCES = ['pv_kernels.hip', 'pv_bls.hip', 'pv_api.cpp']
 COMMON = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-Wall', '-Wno-unused-function',
           '-Wno-unused-variable', '-I' + os.path.join(REPO, 'include')]
 

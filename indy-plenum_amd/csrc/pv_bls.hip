@@ -1,0 +1,509 @@
+// BLS COMMIT check on the GPU -- kernels and C-ABI
+// (include/plenum_verify.h, "BLS COMMIT check").
+//
+// Reference path: every COMMIT's BLS signature is checked by
+//   BlsBftReplicaPlenum.validate_commit -> _validate_signature
+//     (plenum/bls/bls_bft_replica_plenum.py:55-75, 194-213)
+//   -> BlsCryptoVerifierIndyCrypto.verify_sig (crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:73-82)
+//   -> python-ursa Bls.verify: e(sigma, g) == e(H(m), pk) over AMCL BN254.
+// Here one lane runs one check as e(sigma, g) e(-H(m), pk) == 1: a product of
+// two Miller loops over PRECOMPUTED lines of the fixed G2 arguments (the
+// generator and the node keys, k_bls_lines) and one final exponentiation
+// (csrc/pv_bn254.h).  Checks are grouped by key so that each wave reads ONE
+// key's lines (wave-uniform addresses: one L2 line serves 64 lanes), and each
+// distinct message is hashed to G1 once (k_bls_hash).
+//
+// PARITY UNPINNED: ursa / AMCL are absent here and the reference holds no BLS
+// vector; the checker is oracle/bn254_oracle.c.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/plenum_verify.h"
+#include "pv_bn254.h"
+#include "pv_sha256.h"
+
+namespace {
+
+using namespace bn;
+
+constexpr int KEY_LINE_WORDS = N_LINES * LINE_WORDS;   // 2800 words per G2 point
+constexpr int MSG_WORDS = 4 * NL;                        // x_H, y_H, xq(-H), yq(-H)
+constexpr int BLS_BLOCK = 256;
+
+__device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) w[i] = (uint32_t)a.l[i];
+}
+__device__ __forceinline__ fp ld_fp(const uint32_t* w) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = (int32_t)w[i];
+  return r;
+}
+
+// one lane per G2 point: status + the 70 lines of the generator (point 0) and the keys
+__global__ __launch_bounds__(64) void k_bls_lines(const uint8_t* __restrict__ pts, uint32_t n, uint32_t* __restrict__ lines,
+                                                  uint8_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2a q;
+  const int st = g2_decode(pts + 128ull * i, q);
+  status[i] = (uint8_t)st;
+  uint32_t* out = lines + (uint64_t)KEY_LINE_WORDS * i;
+  if (st == 0) {
+    g2_lines(out, q);
+  } else {
+    for (int k = 0; k < KEY_LINE_WORDS; ++k) out[k] = 0;
+  }
+}
+
+// one lane per distinct message: H(m) and (x/y, 1/y) of -H(m)
+__global__ __launch_bounds__(64) void k_bls_hash(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+                                                 uint32_t n, uint32_t* __restrict__ tab) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t d[8];
+  pv::sha256_msg(d, blob + off[i], off[i + 1] - off[i], 0, 0);
+  fp x, y, xq, yq;
+  hash_to_g1(reinterpret_cast<const uint8_t*>(d), x, y);
+  line_point(x, y, true, xq, yq);
+  uint32_t* t = tab + (uint64_t)MSG_WORDS * i;
+  st_fp(t, x);
+  st_fp(t + NL, y);
+  st_fp(t + 2 * NL, xq);
+  st_fp(t + 3 * NL, yq);
+}
+
+// grouping by key: count, padded segment starts (64-aligned), scatter
+__global__ void k_bls_count(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t* __restrict__ cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(cnt + key_idx[i], 1u);
+}
+
+__global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uint32_t* __restrict__ seg,
+                               uint32_t* __restrict__ total) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t s = 0;
+  for (uint32_t j = 0; j < k; ++j) {
+    seg[j] = s;
+    s += (cnt[j] + 63u) & ~63u;
+  }
+  *total = s;
+}
+
+__global__ void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, const uint32_t* __restrict__ seg,
+                              uint32_t* __restrict__ cursor, uint32_t* __restrict__ order) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t key = key_idx[i];
+  order[seg[key] + atomicAdd(cursor + key, 1u)] = (uint32_t)i;
+}
+
+// one lane per check, one key per wave (slots of `order` padded to 64 per key;
+// 0xffffffff = idle lane, which computes on the point at infinity and writes nothing)
+__global__ __launch_bounds__(BLS_BLOCK) void k_bls_verify(
+    const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
+    const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint8_t* __restrict__ verdict) {
+  const uint32_t slot = blockIdx.x * BLS_BLOCK + threadIdx.x;
+  const uint32_t task0 = __builtin_amdgcn_readfirstlane(slot & ~63u);
+  if (task0 >= *total) return;   // whole wave: past the last padded segment
+  const uint32_t j = order[slot];
+  const bool live = j != 0xffffffffu;
+  // lane 0 of a task is always live (segments fill from their start)
+  const uint32_t key = __builtin_amdgcn_readfirstlane(live ? key_idx[j] : 0u);
+  const uint32_t* g_lines = lines;
+  const uint32_t* pk_lines = lines + (uint64_t)KEY_LINE_WORDS * (1 + key);
+  const uint8_t st = kstatus[1 + key];
+  fp xs, ys, xqh = fzero(), yqh = fzero();
+  bool s_inf = true;
+  if (live) {
+    g1_decode(sig + 128ull * j, xs, ys, s_inf);
+    const uint32_t* t = msgtab + (uint64_t)MSG_WORDS * msg_idx[j];
+    if (st == 0) {
+      xqh = ld_fp(t + 2 * NL);
+      yqh = ld_fp(t + 3 * NL);
+    }
+  }
+  const bool ok = bls_check(xs, ys, s_inf, xqh, yqh, st == 1, g_lines, pk_lines);
+  if (live) verdict[j] = (st == 2) ? 0 : (uint8_t)ok;
+}
+
+// data generation: sig[j] = sk[key_idx[j]] * H(msg_idx[j])
+__global__ __launch_bounds__(64) void k_bls_sign(const uint8_t* __restrict__ sks, const uint32_t* __restrict__ msgtab,
+                                                 const uint32_t* __restrict__ msg_idx,
+                                                 const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                 uint8_t* __restrict__ sig) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t* t = msgtab + (uint64_t)MSG_WORDS * msg_idx[j];
+  g1_sign(sig + 128 * j, ld_fp(t), ld_fp(t + NL), sks + 32ull * key_idx[j]);
+}
+
+// pk = sk * g (G2, one lane per key; bench / test data generation)
+__global__ __launch_bounds__(64) void k_bls_pubkeys(const uint8_t* __restrict__ gen, const uint8_t* __restrict__ sks,
+                                                    uint32_t k, uint8_t* __restrict__ pks) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  g2a g;
+  g2_decode(gen, g, false);
+  g2j acc{f2one(), f2one(), f2zero()};
+  const g2j G{g.x, g.y, f2one()};
+  const uint8_t* s = sks + 32ull * i;
+  for (int b = 0; b < 256; ++b) {
+    acc = g2j_dbl(acc);
+    if ((s[b >> 3] >> (7 - (b & 7))) & 1) acc = g2j_add(acc, G);
+  }
+  uint8_t* out = pks + 128ull * i;
+  for (int b = 0; b < 128; ++b) out[b] = 0;
+  if (f2is_zero(acc.z)) return;
+  const fp2 zi = f2inv(acc.z), zi2 = f2sqr(zi);
+  const fp2 x = f2mul(acc.x, zi2), y = f2mul(acc.y, f2mul(zi2, zi));
+  to_be32(out, from_mont(x.a));
+  to_be32(out + 32, from_mont(x.b));
+  to_be32(out + 64, from_mont(y.a));
+  to_be32(out + 96, from_mont(y.b));
+}
+
+// ------------------------------------------------------------------ host side
+thread_local char g_bls_err[512];
+
+int bfail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_bls_err, sizeof g_bls_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define BLS_HIP(expr)                                                                                          \
+  do {                                                                                                         \
+    hipError_t e_ = (expr);                                                                                    \
+    if (e_ != hipSuccess)                                                                                      \
+      return bfail(e_ == hipErrorOutOfMemory ? PV_ENOMEM : PV_EIO, "%s failed: %s (%s:%d)", #expr,             \
+                   hipGetErrorString(e_), __FILE__, __LINE__);                                                 \
+  } while (0)
+
+template <typename T>
+struct Buf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = n < 64 ? 64 : n;
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct BlsDev {
+  int ord = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t nkeys = 0;             // keys in the prepared set (lines of 1 + nkeys points)
+  Buf<uint32_t> lines;
+  Buf<uint8_t> kstatus, pts;
+  // per-call workspaces
+  Buf<uint32_t> msgtab, cnt, seg, cursor, order, total, midx, kidx;
+  Buf<uint8_t> sig, blob, verdict, sks;
+  Buf<uint64_t> off;
+  float ms_hash = 0, ms_verify = 0;
+};
+
+std::mutex g_bls_mu;
+std::vector<BlsDev> g_bls;
+
+int bls_dev(int device, BlsDev** out) {
+  for (auto& d : g_bls)
+    if (d.ord == device) {
+      *out = &d;
+      return PV_OK;
+    }
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+    return bfail(PV_ENODEV, "HIP device %d not available", device);
+  g_bls.emplace_back();
+  BlsDev& d = g_bls.back();
+  d.ord = device;
+  BLS_HIP(hipSetDevice(device));
+  BLS_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  for (auto& e : d.ev) BLS_HIP(hipEventCreate(&e));
+  *out = &d;
+  return PV_OK;
+}
+
+struct Guard {
+  int prev = -1;
+  Guard() { (void)hipGetDevice(&prev); }
+  ~Guard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+// grouping + verify on device buffers, on d.stream (or s)
+int enqueue_verify(BlsDev& d, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n_msgs,
+                   const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n, uint8_t* verdict, hipStream_t s) {
+  if (!d.nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", d.ord);
+  if (n > 0xffffffffull - 64ull * d.nkeys) return bfail(PV_EINVAL, "too many checks in one call");
+  const uint64_t slots = ((n + 63) / 64 + d.nkeys) * 64;
+  BLS_HIP(d.msgtab.ensure(n_msgs * MSG_WORDS));
+  BLS_HIP(d.cnt.ensure(d.nkeys));
+  BLS_HIP(d.cursor.ensure(d.nkeys));
+  BLS_HIP(d.seg.ensure(d.nkeys));
+  BLS_HIP(d.total.ensure(1));
+  BLS_HIP(d.order.ensure(slots));
+  BLS_HIP(hipEventRecord(d.ev[0], s));
+  if (n_msgs) hipLaunchKernelGGL(k_bls_hash, dim3(blocks_for(n_msgs, 64)), dim3(64), 0, s, blob, off, (uint32_t)n_msgs,
+                                 d.msgtab.p);
+  BLS_HIP(hipGetLastError());
+  BLS_HIP(hipEventRecord(d.ev[1], s));
+  BLS_HIP(hipMemsetAsync(d.cnt.p, 0, d.nkeys * 4, s));
+  BLS_HIP(hipMemsetAsync(d.cursor.p, 0, d.nkeys * 4, s));
+  BLS_HIP(hipMemsetAsync(d.order.p, 0xff, slots * 4, s));
+  hipLaunchKernelGGL(k_bls_count, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, d.cnt.p);
+  hipLaunchKernelGGL(k_bls_segments, dim3(1), dim3(64), 0, s, d.cnt.p, d.nkeys, d.seg.p, d.total.p);
+  hipLaunchKernelGGL(k_bls_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, d.seg.p, d.cursor.p,
+                     d.order.p);
+  BLS_HIP(hipGetLastError());
+  BLS_HIP(hipEventRecord(d.ev[2], s));
+  hipLaunchKernelGGL(k_bls_verify, dim3(blocks_for(slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx, key_idx,
+                     d.order.p, d.total.p, d.msgtab.p, d.lines.p, d.kstatus.p, verdict);
+  BLS_HIP(hipGetLastError());
+  BLS_HIP(hipEventRecord(d.ev[3], s));
+  return PV_OK;
+}
+
+int collect_times(BlsDev& d) {
+  BLS_HIP(hipEventSynchronize(d.ev[3]));
+  BLS_HIP(hipEventElapsedTime(&d.ms_hash, d.ev[0], d.ev[1]));
+  BLS_HIP(hipEventElapsedTime(&d.ms_verify, d.ev[2], d.ev[3]));
+  return PV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pv_bls_last_error(void) { return g_bls_err; }
+
+int pv_bls_set_keys(const uint8_t* gen, const uint8_t* pks, uint64_t k, uint8_t* status, int device) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  if (!gen || (k && !pks)) return bfail(PV_EINVAL, "null buffer");
+  if (k > 65535) return bfail(PV_EINVAL, "at most 65535 keys per set (got %llu)", (unsigned long long)k);
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  BLS_HIP(hipSetDevice(device));
+  const uint64_t np = k + 1;
+  BLS_HIP(d->pts.ensure(np * 128));
+  BLS_HIP(d->lines.ensure(np * KEY_LINE_WORDS));
+  BLS_HIP(d->kstatus.ensure(np));
+  BLS_HIP(hipMemcpyAsync(d->pts.p, gen, 128, hipMemcpyHostToDevice, d->stream));
+  if (k) BLS_HIP(hipMemcpyAsync(d->pts.p + 128, pks, k * 128, hipMemcpyHostToDevice, d->stream));
+  hipLaunchKernelGGL(k_bls_lines, dim3(blocks_for(np, 64)), dim3(64), 0, d->stream, d->pts.p, (uint32_t)np, d->lines.p,
+                     d->kstatus.p);
+  BLS_HIP(hipGetLastError());
+  std::vector<uint8_t> st(np);
+  BLS_HIP(hipMemcpyAsync(st.data(), d->kstatus.p, np, hipMemcpyDeviceToHost, d->stream));
+  BLS_HIP(hipStreamSynchronize(d->stream));
+  if (st[0] != 0) {
+    d->nkeys = 0;
+    return bfail(PV_EINVAL, "the generator is not a point of order r on the twist (status %d)", st[0]);
+  }
+  d->nkeys = (uint32_t)k;
+  if (status) memcpy(status, st.data() + 1, k);
+  return PV_OK;
+}
+
+int pv_bls_verify_batch_device(const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n_msgs,
+                               const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n, uint8_t* verdict,
+                               int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  if (n == 0) return PV_OK;
+  if (!sig || !msg_off || !msg_idx || !key_idx || !verdict || (n_msgs && !msg_blob)) return bfail(PV_EINVAL, "null buffer");
+  BLS_HIP(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  if (int rc = enqueue_verify(*d, sig, msg_blob, msg_off, n_msgs, msg_idx, key_idx, n, verdict, s)) return rc;
+  BLS_HIP(hipStreamSynchronize(s));
+  return collect_times(*d);
+}
+
+int pv_bls_verify_batch(const uint8_t* sig, const uint64_t* sig_len, const uint8_t* msg_blob, const uint64_t* msg_off,
+                        uint64_t n_msgs, const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n,
+                        uint8_t* verdict, int device) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  if (n == 0) return PV_OK;
+  if (!sig || !msg_off || !msg_idx || !key_idx || !verdict || (n_msgs && !msg_blob && msg_off[n_msgs] != msg_off[0]))
+    return bfail(PV_EINVAL, "null buffer");
+  if (!d->nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", device);
+  // host-side argument checks: every index in range, offsets non-decreasing
+  for (uint64_t i = 0; i < n_msgs; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return bfail(PV_EINVAL, "msg_off not monotone at %llu", (unsigned long long)i);
+  for (uint64_t j = 0; j < n; ++j) {
+    if (msg_idx[j] >= n_msgs) return bfail(PV_EINVAL, "msg_idx[%llu] = %u out of range", (unsigned long long)j, msg_idx[j]);
+    if (key_idx[j] >= d->nkeys) return bfail(PV_EINVAL, "key_idx[%llu] = %u out of range", (unsigned long long)j, key_idx[j]);
+  }
+  BLS_HIP(hipSetDevice(device));
+  const uint64_t b0 = msg_off[0], bytes = msg_off[n_msgs] - b0;
+  BLS_HIP(d->sig.ensure(n * 128));
+  BLS_HIP(d->blob.ensure(bytes + 64));
+  BLS_HIP(d->off.ensure(n_msgs + 1));
+  BLS_HIP(d->midx.ensure(n));
+  BLS_HIP(d->kidx.ensure(n));
+  BLS_HIP(d->verdict.ensure(n));
+  std::vector<uint64_t> off(n_msgs + 1);
+  for (uint64_t i = 0; i <= n_msgs; ++i) off[i] = msg_off[i] - b0;
+  hipStream_t s = d->stream;
+  BLS_HIP(hipMemcpyAsync(d->sig.p, sig, n * 128, hipMemcpyHostToDevice, s));
+  if (bytes) BLS_HIP(hipMemcpyAsync(d->blob.p, msg_blob + b0, bytes, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemsetAsync(d->blob.p + bytes, 0, 64, s));
+  BLS_HIP(hipMemcpyAsync(d->off.p, off.data(), (n_msgs + 1) * 8, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemcpyAsync(d->midx.p, msg_idx, n * 4, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemcpyAsync(d->kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, s));
+  if (int rc = enqueue_verify(*d, d->sig.p, d->blob.p, d->off.p, n_msgs, d->midx.p, d->kidx.p, n, d->verdict.p, s))
+    return rc;
+  BLS_HIP(hipMemcpyAsync(verdict, d->verdict.p, n, hipMemcpyDeviceToHost, s));
+  BLS_HIP(hipStreamSynchronize(s));
+  // a signature representation that is not 128 bytes does not decode:
+  // bls_from_str returns None and verify_sig returns False
+  if (sig_len)
+    for (uint64_t j = 0; j < n; ++j)
+      if (sig_len[j] != 128) verdict[j] = 0;
+  return collect_times(*d);
+}
+
+int pv_bls_sign_batch_device(const uint8_t* sks, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n_msgs,
+                             const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n, uint8_t* sig, int device,
+                             void* stream) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  if (n == 0) return PV_OK;
+  if (!sks || !msg_off || !msg_idx || !key_idx || !sig || (n_msgs && !msg_blob)) return bfail(PV_EINVAL, "null buffer");
+  BLS_HIP(hipSetDevice(device));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  BLS_HIP(d->msgtab.ensure(n_msgs * MSG_WORDS));
+  hipLaunchKernelGGL(k_bls_hash, dim3(blocks_for(n_msgs, 64)), dim3(64), 0, s, msg_blob, msg_off, (uint32_t)n_msgs,
+                     d->msgtab.p);
+  hipLaunchKernelGGL(k_bls_sign, dim3(blocks_for(n, 64)), dim3(64), 0, s, sks, d->msgtab.p, msg_idx, key_idx, n, sig);
+  BLS_HIP(hipGetLastError());
+  BLS_HIP(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_bls_sign_batch(const uint8_t* sks, uint64_t k, const uint8_t* msg_blob, const uint64_t* msg_off,
+                      uint64_t n_msgs, const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n, uint8_t* sig,
+                      int device) {
+  if (n == 0) return PV_OK;
+  if (!sks || !msg_off || !msg_idx || !key_idx || !sig) return bfail(PV_EINVAL, "null buffer");
+  for (uint64_t i = 0; i < n_msgs; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return bfail(PV_EINVAL, "msg_off not monotone at %llu", (unsigned long long)i);
+  for (uint64_t j = 0; j < n; ++j)
+    if (msg_idx[j] >= n_msgs || key_idx[j] >= k) return bfail(PV_EINVAL, "index out of range at %llu", (unsigned long long)j);
+  Guard gd;
+  Buf<uint8_t> ks, bl, sg;
+  Buf<uint64_t> of;
+  Buf<uint32_t> mi, ki;
+  const uint64_t b0 = msg_off[0], bytes = msg_off[n_msgs] - b0;
+  std::vector<uint64_t> off(n_msgs + 1);
+  for (uint64_t i = 0; i <= n_msgs; ++i) off[i] = msg_off[i] - b0;
+  {
+    std::lock_guard<std::mutex> lk(g_bls_mu);
+    BlsDev* d = nullptr;
+    if (int rc = bls_dev(device, &d)) return rc;
+  }
+  BLS_HIP(hipSetDevice(device));
+  BLS_HIP(ks.ensure(k * 32));
+  BLS_HIP(bl.ensure(bytes + 64));
+  BLS_HIP(sg.ensure(n * 128));
+  BLS_HIP(of.ensure(n_msgs + 1));
+  BLS_HIP(mi.ensure(n));
+  BLS_HIP(ki.ensure(n));
+  BLS_HIP(hipMemcpy(ks.p, sks, k * 32, hipMemcpyHostToDevice));
+  if (bytes) BLS_HIP(hipMemcpy(bl.p, msg_blob + b0, bytes, hipMemcpyHostToDevice));
+  BLS_HIP(hipMemset(bl.p + bytes, 0, 64));
+  BLS_HIP(hipMemcpy(of.p, off.data(), (n_msgs + 1) * 8, hipMemcpyHostToDevice));
+  BLS_HIP(hipMemcpy(mi.p, msg_idx, n * 4, hipMemcpyHostToDevice));
+  BLS_HIP(hipMemcpy(ki.p, key_idx, n * 4, hipMemcpyHostToDevice));
+  int rc = pv_bls_sign_batch_device(ks.p, bl.p, of.p, n_msgs, mi.p, ki.p, n, sg.p, device, nullptr);
+  if (rc == PV_OK) BLS_HIP(hipMemcpy(sig, sg.p, n * 128, hipMemcpyDeviceToHost));
+  ks.release(); bl.release(); sg.release(); of.release(); mi.release(); ki.release();
+  return rc;
+}
+
+int pv_bls_pubkeys(const uint8_t* gen, const uint8_t* sks, uint64_t k, uint8_t* pks, int device) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  if (k == 0) return PV_OK;
+  if (!gen || !sks || !pks) return bfail(PV_EINVAL, "null buffer");
+  BLS_HIP(hipSetDevice(device));
+  Buf<uint8_t> g, s, o;
+  BLS_HIP(g.ensure(128));
+  BLS_HIP(s.ensure(k * 32));
+  BLS_HIP(o.ensure(k * 128));
+  BLS_HIP(hipMemcpyAsync(g.p, gen, 128, hipMemcpyHostToDevice, d->stream));
+  BLS_HIP(hipMemcpyAsync(s.p, sks, k * 32, hipMemcpyHostToDevice, d->stream));
+  hipLaunchKernelGGL(k_bls_pubkeys, dim3(blocks_for(k, 64)), dim3(64), 0, d->stream, g.p, s.p, (uint32_t)k, o.p);
+  BLS_HIP(hipGetLastError());
+  BLS_HIP(hipMemcpyAsync(pks, o.p, k * 128, hipMemcpyDeviceToHost, d->stream));
+  BLS_HIP(hipStreamSynchronize(d->stream));
+  g.release();
+  s.release();
+  o.release();
+  return PV_OK;
+}
+
+int pv_bls_kernel_ms(int device, float* hash_ms, float* verify_ms) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  for (auto& d : g_bls)
+    if (d.ord == device) {
+      if (hash_ms) *hash_ms = d.ms_hash;
+      if (verify_ms) *verify_ms = d.ms_verify;
+      return PV_OK;
+    }
+  return bfail(PV_ENOTINIT, "no BLS state on device %d", device);
+}
+
+void pv_bls_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  for (auto& d : g_bls) {
+    (void)hipSetDevice(d.ord);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    d.lines.release(); d.kstatus.release(); d.pts.release(); d.msgtab.release(); d.cnt.release(); d.seg.release();
+    d.cursor.release(); d.order.release(); d.total.release(); d.midx.release(); d.kidx.release(); d.sig.release();
+    d.blob.release(); d.verdict.release(); d.sks.release(); d.off.release();
+    for (auto& e : d.ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    d.stream = nullptr;
+  }
+  g_bls.clear();
+}
+
+}  // extern "C"

@@ -30,6 +30,16 @@
 #ifndef PV_HD
 #define PV_HD __host__ __device__ __forceinline__
 #endif
+// the heavy building blocks (Fp6 / Fp12 products, squarings, Frobenius maps,
+// exponentiations, point steps) are out-of-line functions: fully inlined, one
+// check is ~10^6 instructions and hipcc takes most of an hour
+#ifndef PV_BN_CALL
+#if defined(__HIPCC__)
+#define PV_BN_CALL __device__ __noinline__
+#else
+#define PV_BN_CALL static __attribute__((noinline))
+#endif
+#endif
 #ifndef PV_BN_CHECK_MUL
 #define PV_BN_CHECK_MUL(a, b)
 #endif
@@ -272,7 +282,7 @@ PV_HD bool lt_p(const fp& x) {
 }
 
 // x^e for a fixed 256-bit exponent (little-endian words, uniform branches)
-PV_HD fp pow_fixed(const fp& x, const uint64_t* e) {
+PV_BN_CALL fp pow_fixed(const fp& x, const uint64_t* e) {
   fp acc = fone(), b = x;
   for (int w = 0; w < 4; ++w) {
     const uint64_t ew = e[w];
@@ -323,7 +333,7 @@ PV_HD fp6 f6sub(const fp6& x, const fp6& y) { return fp6{f2sub(x.c0, y.c0), f2su
 PV_HD fp6 f6neg(const fp6& x) { return fp6{f2neg(x.c0), f2neg(x.c1), f2neg(x.c2)}; }
 PV_HD fp6 f6mulv(const fp6& x) { return fp6{f2mulxi(x.c2), x.c0, x.c1}; }
 // Karatsuba over Fp2 (6 Fp2 products)
-PV_HD fp6 f6mul(const fp6& a, const fp6& b) {
+PV_BN_CALL fp6 f6mul(const fp6& a, const fp6& b) {
   const fp2 v0 = f2mul(a.c0, b.c0), v1 = f2mul(a.c1, b.c1), v2 = f2mul(a.c2, b.c2);
   const fp2 s12 = f2mul(fp2{add(a.c1.a, a.c2.a), add(a.c1.b, a.c2.b)}, fp2{add(b.c1.a, b.c2.a), add(b.c1.b, b.c2.b)});
   const fp2 s01 = f2mul(fp2{add(a.c0.a, a.c1.a), add(a.c0.b, a.c1.b)}, fp2{add(b.c0.a, b.c1.a), add(b.c0.b, b.c1.b)});
@@ -344,7 +354,7 @@ PV_HD fp6 f6mul01(const fp6& x, const fp2& b0, const fp2& b1) {
   r.c2 = f2add(t1, t2);
   return r;
 }
-PV_HD fp6 f6inv(const fp6& x) {
+PV_BN_CALL fp6 f6inv(const fp6& x) {
   const fp2 t0 = f2sub(f2sqr(x.c0), f2mulxi(f2mul(x.c1, x.c2)));
   const fp2 t1 = f2sub(f2mulxi(f2sqr(x.c2)), f2mul(x.c0, x.c1));
   const fp2 t2 = f2sub(f2sqr(x.c1), f2mul(x.c0, x.c2));
@@ -355,22 +365,22 @@ PV_HD fp6 f6inv(const fp6& x) {
 // ------------------------------------------------------------------ Fp12
 PV_HD fp12 f12one() { return fp12{f6one(), f6zero()}; }
 PV_HD fp12 f12conj(const fp12& x) { return fp12{x.a, f6neg(x.b)}; }
-PV_HD fp12 f12mul(const fp12& x, const fp12& y) {   // Karatsuba: 3 Fp6 products
+PV_BN_CALL fp12 f12mul(const fp12& x, const fp12& y) {   // Karatsuba: 3 Fp6 products
   const fp6 t0 = f6mul(x.a, y.a), t1 = f6mul(x.b, y.b);
   const fp6 s = f6mul(f6add(x.a, x.b), f6add(y.a, y.b));
   return fp12{f6add(t0, f6mulv(t1)), f6sub(f6sub(s, t0), t1)};
 }
-PV_HD fp12 f12sqr(const fp12& x) {   // complex squaring: 2 Fp6 products
+PV_BN_CALL fp12 f12sqr(const fp12& x) {   // complex squaring: 2 Fp6 products
   const fp6 t = f6mul(x.a, x.b);
   const fp6 s = f6mul(f6add(x.a, x.b), f6add(x.a, f6mulv(x.b)));
   return fp12{f6sub(f6sub(s, t), f6mulv(t)), f6add(t, t)};
 }
-PV_HD fp12 f12inv(const fp12& x) {
+PV_BN_CALL fp12 f12inv(const fp12& x) {
   const fp6 d = f6inv(f6sub(f6mul(x.a, x.a), f6mulv(f6mul(x.b, x.b))));
   return fp12{f6mul(x.a, d), f6neg(f6mul(x.b, d))};
 }
 // f * (1 + (b0 + b1 v) w): the normalised line (5 + 5 Fp2 products)
-PV_HD fp12 f12mul_line(const fp12& f, const fp2& b0, const fp2& b1) {
+PV_BN_CALL fp12 f12mul_line(const fp12& f, const fp2& b0, const fp2& b1) {
   const fp6 t = f6mul01(f.b, b0, b1);
   const fp6 s = f6mul01(f.a, b0, b1);
   return fp12{f6add(f.a, f6mulv(t)), f6add(f.b, s)};
@@ -388,7 +398,7 @@ PV_HD fp2 frob_c(const fp2& c, int n, const uint32_t* ga, const uint32_t* gb) {
   const fp2 x = (n & 1) ? f2conj(c) : c;
   return f2mul(x, f2cst(ga, gb));
 }
-PV_HD fp12 f12frob1(const fp12& x) {
+PV_BN_CALL fp12 f12frob1(const fp12& x) {
   fp12 r;
   r.a.c0 = f2conj(x.a.c0);
   r.b.c0 = frob_c(x.b.c0, 1, G1_1_A, G1_1_B);
@@ -398,7 +408,7 @@ PV_HD fp12 f12frob1(const fp12& x) {
   r.b.c2 = frob_c(x.b.c2, 1, G1_5_A, G1_5_B);
   return r;
 }
-PV_HD fp12 f12frob2(const fp12& x) {   // gamma_{2,e} in Fp
+PV_BN_CALL fp12 f12frob2(const fp12& x) {   // gamma_{2,e} in Fp
   fp12 r;
   r.a.c0 = x.a.c0;
   r.b.c0 = f2mulfp(x.b.c0, cst(G2_1_A));
@@ -408,7 +418,7 @@ PV_HD fp12 f12frob2(const fp12& x) {   // gamma_{2,e} in Fp
   r.b.c2 = f2mulfp(x.b.c2, cst(G2_5_A));
   return r;
 }
-PV_HD fp12 f12frob3(const fp12& x) {
+PV_BN_CALL fp12 f12frob3(const fp12& x) {
   fp12 r;
   r.a.c0 = f2conj(x.a.c0);
   r.b.c0 = frob_c(x.b.c0, 3, G3_1_A, G3_1_B);
@@ -436,7 +446,7 @@ PV_HD fp2 three_plus_two(const fp2& t, const fp2& z) {    // 3t + 2z
   const fp2 d = f2add(t, z);
   return f2add(f2dbl(d), t);
 }
-PV_HD fp12 cyc_sqr(const fp12& x) {
+PV_BN_CALL fp12 cyc_sqr(const fp12& x) {
   fp2 t0, t1, t2, t3, t4, t5;
   fp4_sqr(t0, t1, x.a.c0, x.b.c1);
   fp4_sqr(t2, t3, x.b.c0, x.a.c2);
@@ -454,8 +464,8 @@ PV_HD fp12 cyc_sqr(const fp12& x) {
 // (the squarings' 3t -/+ 2z feed the input back unreduced: values double per
 // squaring, so every fourth one is followed by a reduction)
 PV_HD fp6 f6reduce(const fp6& x) { return fp6{f2reduce(x.c0), f2reduce(x.c1), f2reduce(x.c2)}; }
-PV_HD fp12 f12reduce(const fp12& x) { return fp12{f6reduce(x.a), f6reduce(x.b)}; }
-PV_HD fp12 cyc_pow_u(const fp12& x) {
+PV_BN_CALL fp12 f12reduce(const fp12& x) { return fp12{f6reduce(x.a), f6reduce(x.b)}; }
+PV_BN_CALL fp12 cyc_pow_u(const fp12& x) {
   fp12 t = x;
   for (int i = 0; i < 7; ++i) {
     t = cyc_sqr(t);
@@ -471,7 +481,7 @@ PV_HD fp12 cyc_pow_u(const fp12& x) {
 }
 
 // f^((p^12 - 1)/r): easy part, then Scott et al.'s hard-part chain
-PV_HD fp12 final_exp(const fp12& f0) {
+PV_BN_CALL fp12 final_exp(const fp12& f0) {
   fp12 f = f12mul(f12conj(f0), f12inv(f0));   // ^(p^6 - 1)
   f = f12mul(f12frob2(f), f);                // ^(p^2 + 1)
   const fp12 fu = cyc_pow_u(f);
@@ -504,7 +514,7 @@ static constexpr int LINE_WORDS = 4 * NL;   // B'.a B'.b C'.a C'.b
 struct g2a {
   fp2 x, y;
 };
-PV_HD void line_affine(uint32_t* out, g2a& T, const g2a& S, bool dbl_step) {
+PV_BN_CALL void line_affine(uint32_t* out, g2a& T, const g2a& S, bool dbl_step) {
   fp2 lam;
   if (dbl_step) {
     const fp2 x2 = f2sqr(T.x);
@@ -524,7 +534,7 @@ PV_HD void line_affine(uint32_t* out, g2a& T, const g2a& S, bool dbl_step) {
 }
 PV_HD bool ate_bit(int i) { return (ATE_LO >> i) & 1; }
 
-PV_HD void g2_lines(uint32_t* out, const g2a& Q) {
+PV_BN_CALL void g2_lines(uint32_t* out, const g2a& Q) {
   g2a T = Q;
   int k = 0;
   for (int i = 63; i >= 0; --i) {
@@ -600,7 +610,7 @@ PV_HD fp sqrt_fp(const fp& a, bool& ok) {
 struct g1j {
   fp x, y, z;
 };
-PV_HD g1j g1j_dbl(const g1j& p) {   // dbl-2009-l
+PV_BN_CALL g1j g1j_dbl(const g1j& p) {   // dbl-2009-l
   const fp A = sqr(p.x), B = sqr(p.y), C = sqr(B);
   const fp D = dbl(subn(subn(sqr(addn(p.x, B)), A), C));
   const fp E = addn(dbl(A), A), F = sqr(E);
@@ -611,7 +621,7 @@ PV_HD g1j g1j_dbl(const g1j& p) {   // dbl-2009-l
   return r;
 }
 // p + q with q affine (madd-2007-bl); p may be the point at infinity (z = 0)
-PV_HD g1j g1j_madd(const g1j& p, const fp& qx, const fp& qy, bool p_inf) {
+PV_BN_CALL g1j g1j_madd(const g1j& p, const fp& qx, const fp& qy, bool p_inf) {
   if (p_inf) return g1j{qx, qy, fone()};
   const fp Z1Z1 = sqr(p.z), U2 = mul(qx, Z1Z1), S2 = mul(qy, mul(p.z, Z1Z1));
   const fp H = subn(U2, p.x), HH = sqr(H), I = dbl(dbl(HH)), J = mul(H, I);
@@ -627,7 +637,7 @@ PV_HD g1j g1j_madd(const g1j& p, const fp& qx, const fp& qy, bool p_inf) {
 struct g2j {
   fp2 x, y, z;
 };
-PV_HD g2j g2j_dbl(const g2j& p) {
+PV_BN_CALL g2j g2j_dbl(const g2j& p) {
   const fp2 A = f2sqr(p.x), B = f2sqr(p.y), C = f2sqr(B);
   const fp2 D = f2dbl(f2sub(f2sub(f2sqr(f2add(p.x, B)), A), C));
   const fp2 E = f2add(f2dbl(A), A), F = f2sqr(E);
@@ -638,7 +648,7 @@ PV_HD g2j g2j_dbl(const g2j& p) {
   return r;
 }
 // full Jacobian addition with every exceptional case (doubling, inverse, infinity)
-PV_HD g2j g2j_add(const g2j& p, const g2j& q) {
+PV_BN_CALL g2j g2j_add(const g2j& p, const g2j& q) {
   if (f2is_zero(p.z)) return q;
   if (f2is_zero(q.z)) return p;
   const fp2 Z1Z1 = f2sqr(p.z), Z2Z2 = f2sqr(q.z);
@@ -657,7 +667,7 @@ PV_HD g2j g2j_add(const g2j& p, const g2j& q) {
   return r;
 }
 // r * Q == O  (Q affine, not O)
-PV_HD bool g2_in_subgroup(const g2a& q) {
+PV_BN_CALL bool g2_in_subgroup(const g2a& q) {
   g2j acc{f2one(), f2one(), f2zero()};
   const g2j Q{q.x, q.y, f2one()};
   for (int w = 3; w >= 0; --w)

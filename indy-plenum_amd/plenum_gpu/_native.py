@@ -68,6 +68,19 @@ SIGNATURES = [
     ('pv_set_lat_kernel', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_set_host_fused', ctypes.c_int, [ctypes.c_int]),
     ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
+    ('pv_bls_set_keys', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    ('pv_bls_verify_batch', ctypes.c_int,
+     [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    ('pv_bls_verify_batch_device', ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp]),
+    ('pv_bls_sign_batch_device', ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp]),
+    ('pv_bls_sign_batch', ctypes.c_int,
+     [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    ('pv_bls_pubkeys', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    ('pv_bls_kernel_ms', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+    ('pv_bls_last_error', ctypes.c_char_p, []),
+    ('pv_bls_shutdown', None, []),
     ('pv_kernel_timing', ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
       ctypes.POINTER(ctypes.c_uint64)]),
@@ -195,6 +208,7 @@ def shutdown():
     with _lock:
         if _lib is not None:
             _lib.pv_shutdown()
+            _lib.pv_bls_shutdown()
         _inited_mask = None
 
 
@@ -299,3 +313,92 @@ def sign_batch_arrays(seeds, blob, off):
     if n:
         _check('pv_sign_batch', load().pv_sign_batch(_ptr(seeds), _ptr(blob), _ptr(off), n, _ptr(pk), _ptr(sig)))
     return pk, sig
+
+
+# ---------------------------------------------------------------- BLS COMMIT check (row f4)
+BLS_KEY_OK, BLS_KEY_INFINITY, BLS_KEY_NOT_IN_G2 = 0, 1, 2
+
+
+def _bls_check(fn, rc):
+    if rc != 0:
+        raise PlenumGpuError(fn, rc, load().pv_bls_last_error().decode(errors='replace'))
+
+
+_bls_owner = {}   # device -> the object whose key set is on the device
+
+
+def bls_keyset_owner(device=0):
+    return _bls_owner.get(device)
+
+
+def bls_set_keys(gen, pks, device=0, owner=None):
+    """pv_bls_set_keys: the generator (128 B) and k keys (k x 128) -> status (k,) u8
+    (0 = in G2, 1 = off the twist, 2 = outside the order-r subgroup).  The device
+    holds ONE key set; `owner` records whose it is (bls_keyset_owner)."""
+    ensure_init()
+    _bls_owner[device] = None
+    gen = np.ascontiguousarray(np.frombuffer(bytes(gen), np.uint8))
+    if gen.size != 128:
+        raise ValueError('the generator representation is 128 bytes')
+    pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(-1, 128)
+    st = np.zeros(pks.shape[0], np.uint8)
+    _bls_check('pv_bls_set_keys', load().pv_bls_set_keys(_ptr(gen), _ptr(pks), pks.shape[0], _ptr(st), device))
+    _bls_owner[device] = owner
+    return st
+
+
+def bls_verify_arrays(sig, blob, off, msg_idx, key_idx, sig_len=None, device=0):
+    """pv_bls_verify_batch over host arrays: sig (n,128) u8, messages (blob, off),
+    msg_idx / key_idx (n,) u32 -> verdict (n,) bool."""
+    ensure_init()
+    sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 128)
+    n = sig.shape[0]
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    msg_idx = np.ascontiguousarray(msg_idx, dtype=np.uint32)
+    key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+    if msg_idx.shape != (n,) or key_idx.shape != (n,):
+        raise ValueError('msg_idx / key_idx must have one entry per signature')
+    sl = None if sig_len is None else np.ascontiguousarray(sig_len, dtype=np.uint64)
+    if sl is not None and sl.shape != (n,):
+        raise ValueError('sig_len must have one entry per signature')
+    verdict = np.zeros(n, np.uint8)
+    if n:
+        _bls_check('pv_bls_verify_batch', load().pv_bls_verify_batch(
+            _ptr(sig), _ptr(sl) if sl is not None else None, _ptr(blob), _ptr(off), off.shape[0] - 1, _ptr(msg_idx),
+            _ptr(key_idx), n, _ptr(verdict), device))
+    return verdict.astype(bool)
+
+
+def bls_sign_arrays(sks, blob, off, msg_idx, key_idx, device=0):
+    """pv_bls_sign_batch: sig j = sk[key_idx[j]] * H(message msg_idx[j]) -> (n, 128) u8 (data generation)."""
+    ensure_init()
+    sks = np.ascontiguousarray(sks, dtype=np.uint8).reshape(-1, 32)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    msg_idx = np.ascontiguousarray(msg_idx, dtype=np.uint32)
+    key_idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+    n = msg_idx.shape[0]
+    out = np.zeros((n, 128), np.uint8)
+    if n:
+        _bls_check('pv_bls_sign_batch', load().pv_bls_sign_batch(
+            _ptr(sks), sks.shape[0], _ptr(blob), _ptr(off), off.shape[0] - 1, _ptr(msg_idx), _ptr(key_idx), n,
+            _ptr(out), device))
+    return out
+
+
+def bls_pubkeys(gen, sks, device=0):
+    """pv_bls_pubkeys: pk = sk * g for k 32-byte big-endian secret scalars (data generation)."""
+    ensure_init()
+    gen = np.ascontiguousarray(np.frombuffer(bytes(gen), np.uint8))
+    sks = np.ascontiguousarray(sks, dtype=np.uint8).reshape(-1, 32)
+    out = np.zeros((sks.shape[0], 128), np.uint8)
+    _bls_check('pv_bls_pubkeys', load().pv_bls_pubkeys(_ptr(gen), _ptr(sks), sks.shape[0], _ptr(out), device))
+    return out
+
+
+def bls_kernel_ms(device=0):
+    """(hash_ms, verify_ms) of the last BLS verify call on `device` (HIP events)."""
+    h, v = ctypes.c_float(), ctypes.c_float()
+    _bls_check('pv_bls_kernel_ms', load().pv_bls_kernel_ms(device, ctypes.byref(h), ctypes.byref(v)))
+    return h.value, v.value

@@ -1,0 +1,267 @@
+"""BLS COMMIT check on the GPU -- drop-in mirror of the
+reference's BLS verifier surface, batched.
+
+Reference path (every COMMIT of every 3PC batch):
+  BlsBftReplicaPlenum.validate_commit (plenum/bls/bls_bft_replica_plenum.py:55-75)
+    -> _validate_signature (:194-213): pk = bls_key_register.get_key_by_name(sender),
+       message = MultiSignatureValue(...).as_single_value()
+    -> BlsCryptoVerifierIndyCrypto.verify_sig (crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:73-82)
+    -> python-ursa Bls.verify(signature, message, pk, generator).
+Here: `BlsCryptoVerifierGpu.verify_sig` keeps that signature and semantics (None
+signature or key -> False) and `verify_sig_batch` runs many checks in ONE GPU
+pass (pv_bls_verify_batch: every message hashed once, checks grouped by key, the
+generator's and keys' lines precomputed once per key set);
+`validate_commit_batch` is `validate_commit`'s rule for a batch of COMMITs, and
+`commit_quorums` feeds the verdicts to the n - f tally kernel (pv_tally_votes,
+ordering_service.py:457-488 rule 3 + models.py voter sets).
+
+PARITY UNPINNED: ursa / Milagro AMCL are not importable here and
+the reference holds no BLS vector.  The generator constant and the message bytes
+(MultiSignatureValue.as_single_value, msgpack of the sorted dict) are the
+reference's own and are pinned by tests/golden/bls.json; the verdicts are pinned
+only against the restatements the tests hold.  No CPU fallback:
+the checks run on the HIP kernels or raise.
+"""
+from collections import OrderedDict, namedtuple
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _native
+from . import base58
+
+GroupParams = namedtuple('GroupParams', 'group_name, g')   # crypto/bls/bls_crypto.py:5-6
+
+# BlsGroupParamsLoaderIndyCrypto.load_group_params (bls_crypto_indy_crypto.py:15-20)
+GENERATOR = ('3LHpUjiyFC2q2hD7MnwwNmVXiuaFbQx2XkAFJWzswCjgN1utjsCeLzHsKk1nJvFEaS4fcrUmVAkdhtPCYbrVyATZcmzwJReTcJq'
+             'wqBCPTmTQ9uWPwz6rEncKb2pYYYFcdHa8N17HzVyTqKfgPi4X9pMetfT3A5xCHq54R2pDNYWVLDX')
+
+CM_BLS_SIG_WRONG = 2          # crypto/bls/bls_bft_replica.py:9
+PPR_BLS_MULTISIG_WRONG = 1    # :8
+REPR_SIZE = 128               # python-ursa's representation size of a G1 / G2 element
+
+
+class BlsGroupParamsLoaderIndyCrypto:
+    def load_group_params(self) -> GroupParams:
+        return GroupParams('generator', GENERATOR)
+
+
+class IndyCryptoError(Exception):
+    """what ursa raises for a representation it cannot parse"""
+
+
+class BlsEntity:
+    """Byte holder with ursa's BlsEntity surface (as_bytes / from_bytes).
+    The curve arithmetic never runs on the host: decoding happens in the kernels."""
+    __slots__ = ('_b',)
+
+    def __init__(self, b: bytes):
+        self._b = bytes(b)
+
+    def as_bytes(self) -> bytes:
+        return self._b
+
+    @classmethod
+    def from_bytes(cls, b):
+        return cls(b)
+
+    def __eq__(self, other):
+        return type(self) is type(other) and self._b == other._b
+
+    def __hash__(self):
+        return hash((type(self).__name__, self._b))
+
+
+class VerKey(BlsEntity):
+    @classmethod
+    def from_bytes(cls, b):
+        if len(b) != REPR_SIZE:
+            raise IndyCryptoError('Invalid len of bytes representation for PointG2')
+        return cls(b)
+
+
+class Generator(VerKey):
+    pass
+
+
+class Signature(BlsEntity):
+    """Any length is carried: a representation that is not 128 bytes fails to
+    decode inside the check (pv_bls_verify_batch sig_len), i.e. verify_sig
+    returns False -- ursa's from_bytes error surfaces the same way (bls_from_str
+    -> None -> False)."""
+
+
+class MultiSignature(Signature):
+    pass
+
+
+class IndyCryptoBlsUtils:
+    """crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:23-66"""
+    SEED_LEN = 32
+
+    @staticmethod
+    def bls_to_str(v: BlsEntity) -> str:
+        return base58.b58encode(v.as_bytes()).decode('utf-8')
+
+    @staticmethod
+    def bls_from_str(v: str, cls) -> Optional[BlsEntity]:
+        try:
+            bts = base58.b58decode(v)
+        except ValueError:
+            return None
+        try:
+            return cls.from_bytes(bts)
+        except IndyCryptoError:
+            return None
+
+    @staticmethod
+    def bls_pk_from_str(v: str) -> Optional[VerKey]:
+        return IndyCryptoBlsUtils.bls_from_str(v, VerKey)
+
+
+class PlenumTypeError(TypeError):
+    """common/exceptions.py:16-33 (message format kept)"""
+
+    def __init__(self, v_name, v_value, v_exp_t):
+        super().__init__("variable '{}', type {}, expected: {}".format(v_name, type(v_value), v_exp_t))
+
+
+class MultiSignatureValue:
+    """crypto/bls/bls_multi_signature.py:7-81: the value a COMMIT's BLS signature
+    covers; as_single_value() = msgpack of the field dict sorted by key
+    (multi_signature_value_serializer = MsgPackSerializer,
+    common/serializers/serialization.py:21, msgpack_serializer.py:21-31)."""
+
+    def __init__(self, ledger_id: int, state_root_hash: str, pool_state_root_hash: str, txn_root_hash: str,
+                 timestamp: int):
+        for name, val, t in (('ledger_id', ledger_id, int), ('state_root_hash', state_root_hash, str),
+                             ('pool_state_root_hash', pool_state_root_hash, str),
+                             ('txn_root_hash', txn_root_hash, str), ('timestamp', timestamp, int)):
+            if not isinstance(val, t):
+                raise PlenumTypeError(name, val, t)
+        self.ledger_id = ledger_id
+        self.state_root_hash = state_root_hash
+        self.pool_state_root_hash = pool_state_root_hash
+        self.txn_root_hash = txn_root_hash
+        self.timestamp = timestamp
+
+    def as_dict(self):
+        return OrderedDict(sorted(self.__dict__.items()))
+
+    def as_single_value(self) -> bytes:
+        import msgpack
+        return msgpack.packb(self.as_dict(), use_bin_type=True)
+
+    def as_list(self):
+        return [self.ledger_id, self.state_root_hash, self.pool_state_root_hash, self.txn_root_hash, self.timestamp]
+
+    def __eq__(self, other):
+        return isinstance(other, MultiSignatureValue) and self.as_dict() == other.as_dict()
+
+    def __str__(self):
+        return str(self.as_dict())
+
+
+class BlsCryptoVerifierGpu:
+    """BlsCryptoVerifierIndyCrypto (bls_crypto_indy_crypto.py:69-106) with a batch
+    entry point.  Keys are prepared on the device the first time they are seen
+    (pv_bls_set_keys: the generator + every key so far; a pool's node keys are
+    prepared once)."""
+
+    def __init__(self, params: GroupParams, device: int = 0):
+        self._generator = IndyCryptoBlsUtils.bls_from_str(params.g, Generator)
+        if self._generator is None:
+            raise ValueError('bad BLS group generator')
+        self._device = device
+        self._keys = {}          # pk bytes -> index in the device key set
+        self._status = []
+
+    # -- key set
+    def _key_indices(self, pks):
+        new = [b for b in dict.fromkeys(pks) if b not in self._keys]
+        # the device holds one key set: re-prepare when it is not ours any more
+        if new or _native.bls_keyset_owner(self._device) is not self:
+            allk = list(self._keys) + new
+            st = _native.bls_set_keys(self._generator.as_bytes(), np.frombuffer(b''.join(allk), np.uint8),
+                                      device=self._device, owner=self)
+            self._keys = {b: i for i, b in enumerate(allk)}
+            self._status = list(st)
+        return [self._keys[b] for b in pks]
+
+    def key_status(self, pk: VerKey) -> int:
+        """PV_BLS_KEY_OK / _INFINITY / _NOT_IN_G2 of a key (prepares it)"""
+        return int(self._status[self._key_indices([pk.as_bytes()])[0]])
+
+    # -- checks
+    def verify_sig_batch(self, items) -> np.ndarray:
+        """items: [(signature: str, message: bytes, bls_pk: VerKey | None)] ->
+        bool array, entry i == verify_sig(*items[i])."""
+        n = len(items)
+        out = np.zeros(n, bool)
+        rows, sigs, sig_len, msgs, pks = [], [], [], {}, []
+        for i, (signature, message, bls_pk) in enumerate(items):
+            s = IndyCryptoBlsUtils.bls_from_str(signature, Signature)
+            if s is None or bls_pk is None:
+                continue
+            b = s.as_bytes()
+            rows.append(i)
+            sig_len.append(len(b))
+            sigs.append(b[:REPR_SIZE].ljust(REPR_SIZE, b'\0'))
+            msgs.setdefault(bytes(message), len(msgs))
+            pks.append(bls_pk.as_bytes())
+        if not rows:
+            return out
+        kidx = np.array(self._key_indices(pks), np.uint32)
+        midx = np.array([msgs[bytes(items[i][1])] for i in rows], np.uint32)
+        blob, off = _native.pack_messages(list(msgs))
+        got = _native.bls_verify_arrays(np.frombuffer(b''.join(sigs), np.uint8), blob, off, midx, kidx,
+                                        sig_len=np.array(sig_len, np.uint64), device=self._device)
+        out[np.array(rows)] = got
+        return out
+
+    def verify_sig(self, signature: str, message: bytes, bls_pk: Optional[VerKey]) -> bool:
+        return bool(self.verify_sig_batch([(signature, message, bls_pk)])[0])
+
+    def verify_multi_sig(self, signature: str, message: bytes, pks: Sequence[Optional[VerKey]]) -> bool:
+        raise NotImplementedError('multi-signature verification (PRE-PREPARE path) is not on the GPU path; '
+                                  'see DESIGN.md §9')
+
+    # -- COMMITs
+    def validate_commit_batch(self, commits) -> list:
+        """validate_commit's BLS rule for many COMMITs (bls_bft_replica_plenum.py:55-75).
+
+        commits: [(bls_pk VerKey | None, bls_sigs {ledger_id: sig str} | None,
+                   values {ledger_id: MultiSignatureValue})] where `values` holds
+        the MultiSignatureValue _validate_signature builds for each ledger the
+        audit transaction covers.  -> per COMMIT: None (no BLS_SIGS, or every
+        signature verifies) or CM_BLS_SIG_WRONG."""
+        items, owner = [], []
+        res = [None] * len(commits)
+        for c, (pk, sigs, values) in enumerate(commits):
+            if sigs is None:
+                continue
+            for lid, sig in sigs.items():
+                v = values.get(int(lid))
+                if v is None:                      # ledger not in the audit txn
+                    res[c] = CM_BLS_SIG_WRONG
+                    continue
+                items.append((sig, v.as_single_value(), pk))
+                owner.append(c)
+        if items:
+            ok = self.verify_sig_batch(items)
+            for c, good in zip(owner, ok):
+                if not good:
+                    res[c] = CM_BLS_SIG_WRONG
+        return res
+
+
+def commit_quorums(verdicts, senders, batch_off, n_nodes, quorum):
+    """n - f COMMIT quorum per 3PC batch from per-COMMIT verdicts (True = the
+    COMMIT counts) and sender indices, on the tally kernel (voter SET semantics,
+    plenum/server/models.py:16-114): -> (votes, reached)."""
+    return _native.tally_arrays(np.asarray(verdicts, np.uint8), senders, batch_off, n_nodes, quorum)
+
+
+__all__ = ['GroupParams', 'GENERATOR', 'BlsGroupParamsLoaderIndyCrypto', 'IndyCryptoError', 'BlsEntity', 'VerKey',
+           'Generator', 'Signature', 'MultiSignature', 'IndyCryptoBlsUtils', 'MultiSignatureValue',
+           'BlsCryptoVerifierGpu', 'CM_BLS_SIG_WRONG', 'PPR_BLS_MULTISIG_WRONG', 'commit_quorums']

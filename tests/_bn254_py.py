@@ -459,3 +459,37 @@ def verify_sig(sig128, msg, pk128, gen128):
     pk = g2_from_bytes(pk128)
     h = hash_to_g1(msg)
     return pairing_naive(s, g) == pairing_naive(h, pk)
+
+
+def f2_sqrt(a):
+    """a square root of a in Fp2 (None if a is not a square), p = 3 mod 4
+    (test data generation: points on the twist outside G2)"""
+    if a.is_zero():
+        return F2_0
+    # a^((p^2 - 1)/2) == 1 <=> square; for p = 3 mod 4 use the norm method
+    n = (a.a * a.a + a.b * a.b) % P
+    if not is_qr(n):
+        return None
+    s = sqrt_fp(n)
+    for sn in (s, (-s) % P):
+        t = (a.a + sn) * inv(2) % P
+        if is_qr(t):
+            x = sqrt_fp(t)
+            y = a.b * inv(2 * x) % P if x else 0
+            r = F2(x, y)
+            if r * r == a:
+                return r
+    return None
+
+
+def twist_point_outside_g2(seed=1):
+    """a point on E' (y^2 = x^3 + 2/xi) whose order is not r"""
+    x0 = seed
+    while True:
+        x = F2(x0, 1)
+        y = f2_sqrt(x * x * x + BT)
+        if y is not None:
+            q = (x, y)
+            if g2_mul(q, R) is not None:
+                return q
+        x0 += 1
