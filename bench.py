@@ -108,30 +108,80 @@ def _traffic_per_launch():
         return None
 
 
+# SURVEY.md 8(d)'s second work term, W_valu, ALGORITHMIC:
+# the non-MAD operations the curve stage's algorithm needs per half-size verify,
+# counted per primitive on the host build of the kernel code (tools/hostcheck op
+# counters; pinned by tests/test_hostcheck.py::test_op_counts_pin_valu_constants)
+# times each primitive's instruction cost in the radix-2^25.5 field code, split
+# by issue class:
+#   fe_mul   9 x 19 g_j (v_mul_u32_u24) + 10 column carries (v_lshrrev_b64) + the
+#            x19 wrap -> 20 half-rate; 5 x 2 f_odd + 10 masks + 2 adds -> 17 full-rate
+#   fe_sq    5 x 19 f + 10 carries + wrap -> 16 half; 9 x 2 f + 10 masks + 2 -> 21 full
+#   fe_add   10 full; fe_sub / fe_neg 20 full (+2p, -g); fe_carry 30 full (shift, mask, add)
+#   SHA-512  per block 80 rounds x 27 (12 v_alignbit, 8 v_bitop3, 7 64-bit adds)
+#            + 64 schedule words x 19 = 3376 half-rate
+W_ADD_PER_VERIFY, W_SUB_PER_VERIFY, W_CARRY_PER_VERIFY = 723, 778, 164
+SHA512_BLOCKS_C2 = 3          # |R||A||M| = 320 B
+HALF_COST = {'mul': 20, 'sq': 16, 'sha_block': 3376}
+FULL_COST = {'mul': 17, 'sq': 21, 'add': 10, 'sub': 20, 'carry': 30}
+W_HALF_PER_VERIFY = (HALF_COST['mul'] * W_MUL_PER_VERIFY + HALF_COST['sq'] * W_SQ_PER_VERIFY
+                     + HALF_COST['sha_block'] * SHA512_BLOCKS_C2)
+W_FULL_PER_VERIFY = (FULL_COST['mul'] * W_MUL_PER_VERIFY + FULL_COST['sq'] * W_SQ_PER_VERIFY
+                     + FULL_COST['add'] * W_ADD_PER_VERIFY + FULL_COST['sub'] * W_SUB_PER_VERIFY
+                     + FULL_COST['carry'] * W_CARRY_PER_VERIFY)
+
+
+def _class_rates(peak):
+    """Issue rates of the half-rate class (64-bit shifts / adds, v_alignbit,
+    v_mul_u32_u24, v_add_co) and of full-rate 32-bit VALU, as ratios to
+    v_mad_u64_u32 measured in ONE micro-benchmark run (profiles/r01_int_rates.json)
+    scaled to the best MAD ceiling `peak`."""
+    path = os.path.join(REPO, 'profiles', 'r01_int_rates.json')
+    with open(path) as fh:
+        r = {x['insn']: float(x['lane_ops_per_s']) for x in json.load(fh)['results']}
+    mad = r['v_mad_u64_u32']
+    half = sum(r[k] for k in ('v_alignbit_b32', 'v_lshrrev_b64', 'v_lshl_add_u64', 'v_mul_u32_u24', 'v_add_co_u32')) / 5
+    full = (r['v_add_u32'] + r['v_xor_b32']) / 2
+    return peak * half / mad, peak * full / mad
+
+
 def _combined_issue(kernel_rate, peak):
-    """SURVEY.md 8(d)'s integer-ALU roofline, 1 / (W_mad/P_mad + W_valu/P_valu), for
-    the C2 curve kernel: W_valu = the non-MAD VALU lane-ops the kernel executes per
-    verify (rocprofv3 SQ_INSTS_VALU of the C2 launch minus its MAD instructions,
-    profiles/r02_curve_pmc.json), P_valu = 2 x the measured MAD ceiling (full-rate
-    32-bit VALU issues at twice the half-rate v_mad_u64_u32).  A secondary figure:
-    `frac` above prices the MAD work alone."""
-    path = os.path.join(REPO, 'profiles', 'r02_curve_pmc.json')
+    """SURVEY.md 8(d)'s integer-ALU roofline for the C2 curve kernel,
+    1 / (W_mad/P_mad + W_half/P_half + W_full/P_full), every W from the algorithm
+    (constants above, pinned by host op counts) and every P measured (the MAD
+    ceiling; the other two classes at their measured ratios to it).  Beside it,
+    `issue_efficiency` prices the instructions the kernel actually EXECUTES
+    (rocprofv3 SQ_INSTS_VALU, profiles/r02_curve_pmc.json) the same way."""
     try:
+        p_half, p_full = _class_rates(peak)
+    except (OSError, KeyError, ValueError):
+        return None
+    t = W_MAD_PER_VERIFY / peak + W_HALF_PER_VERIFY / p_half + W_FULL_PER_VERIFY / p_full
+    rate = 1.0 / t
+    out = {'model': 'SURVEY.md 8(d): 1 / (W_mad/P_mad + W_half/P_half + W_full/P_full), algorithmic W',
+           'w_mad_per_verify': W_MAD_PER_VERIFY, 'w_half_per_verify': int(W_HALF_PER_VERIFY),
+           'w_full_per_verify': int(W_FULL_PER_VERIFY), 'p_mad': round(peak / 1e12, 3),
+           'p_half': round(p_half / 1e12, 3), 'p_full': round(p_full / 1e12, 3), 'unit': 'T lane-ops/s',
+           'roofline_verifies_per_s': round(rate, 1), 'frac': round(kernel_rate / rate, 4),
+           'source': 'W from tools/hostcheck op counters x per-primitive costs (bench.py); '
+                     'P ratios from profiles/r01_int_rates.json'}
+    try:
+        path = os.path.join(REPO, 'profiles', 'r02_curve_pmc.json')
         with open(path) as fh:
             d = json.load(fh)
         insts = float(d['kernels'][d['curve_kernel']]['SQ_INSTS_VALU'])
         n, deferred = int(d['c2_signatures']), int(d['c2_deferred'])
+        mad_lane_ops = W_MAD_PER_VERIFY * (n - deferred) + W_MAD_FULL * deferred
+        other = (insts * 64 - mad_lane_ops) / n
+        # executed non-MAD instructions priced at the half-rate class (the
+        # bulk of them: 64-bit shifts, v_mul_u32_u24, add-with-carry)
+        rate_exec = 1.0 / (W_MAD_PER_VERIFY / peak + other / p_half)
+        out['issue_efficiency'] = {'executed_non_mad_per_verify': round(other), 'rate_at_executed_work': round(rate_exec, 1),
+                                   'frac': round(kernel_rate / rate_exec, 4),
+                                   'source': 'rocprofv3 SQ_INSTS_VALU of the C2 curve launch (profiles/r02_curve_pmc.json)'}
     except (OSError, KeyError, ValueError):
-        return None
-    mad_lane_ops = W_MAD_PER_VERIFY * (n - deferred) + W_MAD_FULL * deferred
-    w_valu = (insts * 64 - mad_lane_ops) / n
-    p_valu = 2 * peak
-    rate = 1.0 / (W_MAD_PER_VERIFY / peak + w_valu / p_valu)
-    return {'model': 'SURVEY.md 8(d): 1 / (W_mad/P_mad + W_valu/P_valu)', 'w_mad_per_verify': W_MAD_PER_VERIFY,
-            'w_valu_per_verify': round(w_valu), 'p_mad': round(peak / 1e12, 3), 'p_valu': round(p_valu / 1e12, 3),
-            'unit': 'T lane-ops/s', 'roofline_verifies_per_s': round(rate, 1),
-            'frac': round(kernel_rate / rate, 4),
-            'source': 'W_valu from rocprofv3 SQ_INSTS_VALU of the C2 curve launch (profiles/r02_curve_pmc.json)'}
+        pass
+    return out
 
 
 def cpu_baseline(batch, workload, seconds=1.5, sample=8192):

@@ -500,7 +500,7 @@ static constexpr uint32_t P2_O = 2u * ((1u << 25) - 1);
 
 // h = f - g + 2p ; g must be TIGHT.  LOOSE result when f is TIGHT.
 PV_HD void fe_sub(fe& h, const fe& f, const fe& g) {
-  PV_COUNT(add);
+  PV_COUNT(sub);
   h.v[0] = f.v[0] + P2_0 - g.v[0];
 #pragma unroll
   for (int i = 1; i < 10; ++i) h.v[i] = f.v[i] + ((i & 1) ? P2_O : P2_E) - g.v[i];
@@ -508,7 +508,7 @@ PV_HD void fe_sub(fe& h, const fe& f, const fe& g) {
 
 // h = f - g + 4p ; g may be LOOSE up to 2^28 / 2^27.  Result needs fe_carry.
 PV_HD void fe_sub4(fe& h, const fe& f, const fe& g) {
-  PV_COUNT(add);
+  PV_COUNT(sub);
   h.v[0] = f.v[0] + 2u * P2_0 - g.v[0];
 #pragma unroll
   for (int i = 1; i < 10; ++i) h.v[i] = f.v[i] + 2u * ((i & 1) ? P2_O : P2_E) - g.v[i];
@@ -516,7 +516,7 @@ PV_HD void fe_sub4(fe& h, const fe& f, const fe& g) {
 
 // -f = 2p - f (f TIGHT) -> LOOSE
 PV_HD void fe_neg(fe& h, const fe& f) {
-  PV_COUNT(add);
+  PV_COUNT(sub);
   h.v[0] = P2_0 - f.v[0];
 #pragma unroll
   for (int i = 1; i < 10; ++i) h.v[i] = ((i & 1) ? P2_O : P2_E) - f.v[i];

@@ -44,7 +44,7 @@ def hc_verify(hc, pk, sig, blob, off):
 
 
 def counts(hc):
-    c = np.zeros(6, np.uint64)
+    c = np.zeros(7, np.uint64)
     bad = hc.hc_get_counts(_p(c))
     return c, bad
 
@@ -172,6 +172,23 @@ def test_op_counts_pin_bench_constants(hc):
     assert ok.all() and nd == n
     assert int(c[1]) == int(bench.W_SQ_FULL * n)
     assert abs(int(c[0]) / n - bench.W_MUL_FULL) <= 0.5
+
+
+def test_op_counts_pin_valu_constants(hc):
+    """The algorithmic non-MAD work of the roofline's combined figure
+    (bench.W_ADD / W_SUB / W_CARRY_PER_VERIFY, SHA512_BLOCKS_C2), counted on the
+    exact kernel schedule of a half-size verify with a 256-byte message."""
+    import bench
+    n = 32
+    pk, sig, blob, off = _signed_batch(n, 3)
+    ok, c, nd = _run_mode(hc, pk, sig, blob, off, False)
+    assert ok.all() and nd == 0
+    # the conditional sqrt(-1) multiply of the decompressions adds one fe_add
+    assert abs(int(c[2]) / n - bench.W_ADD_PER_VERIFY) <= 1.0
+    assert int(c[6]) == bench.W_SUB_PER_VERIFY * n
+    assert abs(int(c[3]) / n - bench.W_CARRY_PER_VERIFY) <= 1.0
+    assert int(c[4]) == bench.SHA512_BLOCKS_C2 * n
+    assert bench.W_HALF_PER_VERIFY > 0 and bench.W_FULL_PER_VERIFY > 0
 
 
 def test_op_counts_pin_grouped_constants(hc):

@@ -13,7 +13,7 @@
 #include <string.h>
 
 static uint64_t g_cnt[8];
-enum { HC_mul, HC_sq, HC_add, HC_carry, HC_sha, HC_sc };
+enum { HC_mul, HC_sq, HC_add, HC_carry, HC_sha, HC_sc, HC_sub };
 static int g_bad_bound = 0;
 
 #define PV_HD static inline
@@ -286,7 +286,7 @@ void hc_reset_counts(void) {
 
 // counts[0..5] = mul, sq, add, carry, sha blocks, scalar reductions
 int hc_get_counts(uint64_t* counts) {
-  for (int i = 0; i < 6; ++i) counts[i] = g_cnt[i];
+  for (int i = 0; i < 7; ++i) counts[i] = g_cnt[i];
   return g_bad_bound;
 }
 
