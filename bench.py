@@ -86,6 +86,17 @@ W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
 P_MAD_PER_S = 3.3896e13
 
 
+# BLS COMMIT check (row f4, --config c3bls): Fp multiplies / squarings of ONE
+# check as k_bls_verify runs it (sigma decoding, the two-pairing Miller product
+# over precomputed lines, the final exponentiation), counted by the host build
+# of csrc/pv_bn254.h (tests/test_bls_oracle.py::test_check_op_counts_pin_bench);
+# a 254-bit Montgomery multiply in 10 x 28-bit limbs is 100 + 80 v_mad_i64_i32
+# (p's limbs 1 and 3 are zero), a squaring 55 + 80.
+BLS_W_MUL, BLS_W_SQR = 11895, 510
+BLS_MAD_MUL, BLS_MAD_SQR = 180, 135
+BLS_W_MAD = BLS_W_MUL * BLS_MAD_MUL + BLS_W_SQR * BLS_MAD_SQR
+
+
 def _mad_peak():
     """Best v_mad_u64_u32 lane-ops/s over 1..8 waves/SIMD (tools/ubench/mad_peak.hip,
     profiles/r01_mad_peak.json): the chip's integer multiply-add issue ceiling."""
@@ -405,6 +416,126 @@ def main_c1(args):
     return 0 if mism == 0 else 3
 
 
+def main_bls(args):
+    """Row f4: the BLS COMMIT check of a 25-node pool (C3's shape): every node's
+    COMMIT of every 3PC batch carries a BLS signature over that batch's
+    MultiSignatureValue (plenum/bls/bls_bft_replica_plenum.py:194-213); a step
+    verifies all of them (pv_bls_verify_batch_device: hash each message once,
+    group by key, one two-pairing check per COMMIT) and tallies the n - f COMMIT
+    quorum per batch over the COMMITs that pass (pv_tally_votes_device).
+    Synthetic keys/messages; signatures made on the GPU; ~5 % corrupted."""
+    import hashlib
+    from plenum_gpu import base58
+    from plenum_gpu.bls import GENERATOR, MultiSignatureValue
+    from plenum_gpu.device import _p, _stream
+    nn = 25
+    nb = (args.n or 2_500_000) // nn
+    n = nb * nn
+    q = Quorums(nn).commit.value
+    torch.cuda.set_device(0)
+    dev = torch.device('cuda', 0)
+    nat.ensure_init(1)
+    lib = nat.load()
+    r_order = 0x2523648240000001ba344d8000000007ff9f800000000010a10000000000000d
+    sks = np.frombuffer(b''.join((int.from_bytes(hashlib.sha256(b'plenum-gpu/bls-node' + bytes([i])).digest(), 'big')
+                                  % r_order).to_bytes(32, 'big') for i in range(nn)), np.uint8).reshape(nn, 32)
+    gen = base58.b58decode(GENERATOR)
+    pks = nat.bls_pubkeys(gen, sks)
+    assert not nat.bls_set_keys(gen, pks).any()
+
+    def root(tag, b):
+        return base58.b58encode(hashlib.sha256(tag + b.to_bytes(8, 'little')).digest()).decode()
+    msgs = [MultiSignatureValue(1, root(b'state', b), root(b'pool', b // 100), root(b'txn', b), 1700000000 + b)
+            .as_single_value() for b in range(nb)]
+    blob_h, off_h = nat.pack_messages(msgs)
+    blob = torch.zeros(blob_h.size + 64, dtype=torch.uint8, device=dev)
+    blob[:blob_h.size] = torch.from_numpy(blob_h.copy()).to(dev)
+    off = torch.from_numpy(off_h.astype(np.int64)).to(dev)
+    midx = torch.arange(nb, dtype=torch.int32, device=dev).repeat_interleave(nn)
+    kidx = torch.arange(nn, dtype=torch.int32, device=dev).repeat(nb)
+    sig = torch.empty((n, 128), dtype=torch.uint8, device=dev)
+    sk_d = torch.from_numpy(sks.copy()).to(dev)
+    nat._bls_check('pv_bls_sign_batch_device', lib.pv_bls_sign_batch_device(
+        _p(sk_d), _p(blob), _p(off), nb, _p(midx), _p(kidx), n, _p(sig), 0, _stream(dev)))
+    # ~5 % corrupted: half a flipped bit of x (decodes to O), half another batch's signature
+    g = torch.Generator(device=dev)
+    g.manual_seed(41)
+    bad = torch.rand(n, device=dev, generator=g) < 0.05
+    bidx = torch.nonzero(bad).flatten()
+    half = bidx[: bidx.numel() // 2]
+    sig[half, 7] ^= 0x10
+    other = bidx[bidx.numel() // 2:]
+    sig[other] = sig[(other + nn) % n]
+    expect = ~bad
+    sender = kidx.clone()
+    batch_off = torch.arange(nb + 1, dtype=torch.int64, device=dev) * nn
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    votes = torch.empty(nb, dtype=torch.int32, device=dev)
+    reached = torch.empty(nb, dtype=torch.uint8, device=dev)
+
+    def step():
+        nat._bls_check('pv_bls_verify_batch_device', lib.pv_bls_verify_batch_device(
+            _p(sig), _p(blob), _p(off), nb, _p(midx), _p(kidx), n, _p(verdict), 0, _stream(dev)))
+        tally_device(verdict, sender, batch_off, nn, q, votes, reached)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    hash_ms = verify_ms = 0.0
+    for _ in range(args.steps):
+        step()
+        h, v = nat.bls_kernel_ms(0)
+        hash_ms += h
+        verify_ms += v
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    got = verdict.bool()
+    mism = int((got != expect).sum().item())
+    want_votes = expect.view(nb, nn).sum(1)
+    q_mism = int(((want_votes >= q) != reached.bool()).sum().item()) + int((want_votes != votes).sum().item())
+    value = n * args.steps / elapsed
+    verify_ms /= args.steps
+    hash_ms /= args.steps
+    peak = _mad_peak()
+    achieved = BLS_W_MAD * n / (verify_ms * 1e-3)
+    out = {
+        'metric': 'BLS COMMIT checks/sec (verify_sig over AMCL BN254, row f4) on 1 MI355X', 'value': round(value, 1),
+        'unit': 'checks/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'i32 limbs (GF(p) 254-bit, v_mad_i64_i32)',
+        'data': 'synthetic: 25 node keys, one MultiSignatureValue per 3PC batch, signatures made on the GPU, '
+                '~5% corrupted; parity UNPINNED (ursa absent), verdicts checked against the synthetic spec',
+        'config': {'workload': 'C3-BLS: 25-node pool (f=8), {} 3PC batches, every COMMIT BLS-verified + n-f tally'
+                   .format(nb), 'name': 'c3bls', 'checks': n, 'batches': nb},
+        'verdict_mismatches': mism, 'quorum_mismatches': q_mism, 'quorums_reached': int(reached.sum().item()),
+        'kernel_ms': {'hash': round(hash_ms, 3), 'verify': round(verify_ms, 3)},
+        'roofline': {'bound': 'valu', 'kernel': 'k_bls_verify', 'achieved': round(achieved / 1e12, 3),
+                     'peak': round(peak / 1e12, 3), 'unit': 'T v_mad lane-ops/s', 'frac': round(achieved / peak, 4),
+                     'work_per_check': BLS_W_MAD, 'traffic': None,
+                     'note': 'W = {} Fp mul x 180 + {} sqr x 135 v_mad_i64_i32 per check (host op counts)'
+                             .format(BLS_W_MUL, BLS_W_SQR)},
+    }
+    if not args.no_cpu_baseline:
+        orc = ctypes.CDLL(os.path.join(REPO, 'oracle', 'libbls_oracle.so'))
+        sample = 2000
+        threads = min(16, os.cpu_count() or 1)
+        sig_h = np.ascontiguousarray(sig[:sample].cpu().numpy())
+        mi = np.ascontiguousarray(midx[:sample].cpu().numpy().astype(np.uint32))
+        ki = np.ascontiguousarray(kidx[:sample].cpu().numpy().astype(np.uint32))
+        blob16 = np.concatenate([blob_h, np.zeros(16, np.uint8)])
+        res = np.zeros(sample, np.uint8)
+        pp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+        t0 = time.perf_counter()
+        orc.bls_oracle_verify_batch(pp(sig_h), None, pp(blob16), pp(off_h), pp(mi), pp(ki), pp(np.ascontiguousarray(pks)),
+                                    gen, ctypes.c_uint64(sample), pp(res), threads)
+        dt = time.perf_counter() - t0
+        out['cpu_baseline'] = {'value': round(sample / dt, 1), 'unit': 'checks/s', 'cores': threads, 'kind': 'port',
+                               'sample': '{} checks of this workload, oracle/bn254_oracle.c (2 pairings per check, '
+                                         'as ursa) on {} host threads'.format(sample, threads),
+                               'agrees_with_gpu': bool((res.astype(bool) == got[:sample].cpu().numpy()).all())}
+    print(json.dumps(out), flush=True)
+
+
 def main_f3(args):
     """Row f3: ledger Merkle tree hash (leaf SHA-256 + RFC 6962 levels) of 1M x 256 B
     leaves resident in HBM, vs the same tree hash with hashlib on one host thread."""
@@ -550,7 +681,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', choices=sorted(CONFIGS) + ['f3'], default='c2',
+    ap.add_argument('--config', choices=sorted(CONFIGS) + ['f3', 'c3bls'], default='c2',
                     help='workload (default c2, the headline; f3 = ledger Merkle hashing)')
     ap.add_argument('--n', '--count', dest='n', type=int, default=None,
                     help='signatures per GPU (default: the config\'s); spell it --count under torch.distributed.run')
@@ -564,6 +695,8 @@ def main():
     args = ap.parse_args()
     if args.config == 'c1':
         return main_c1(args)
+    if args.config == 'c3bls':
+        return main_bls(args)
     if args.config == 'f3':
         return main_f3(args)
 

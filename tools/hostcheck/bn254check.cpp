@@ -112,6 +112,28 @@ int bnc_verify(const uint8_t* sig128, const uint8_t* m, uint64_t n, const uint8_
   return bls_check(xs, ys, s_inf, xqh, yqh, st == 1, gl, pl) ? 1 : 0;
 }
 
+// the Fp multiplies / squarings of ONE check as k_bls_verify runs it (sigma
+// decoding + bls_check; the lines and H(m) are per key / per message and are
+// prepared before the counters are reset): out = {mul, sqr}
+int bnc_check_counts(const uint8_t* sig128, const uint8_t* m, uint64_t n, const uint8_t* pk128, const uint8_t* gen128,
+                     uint64_t* out) {
+  static uint32_t gl[N_LINES * LINE_WORDS], pl[N_LINES * LINE_WORDS];
+  if (bnc_g2_lines(gen128, gl) != 0 || bnc_g2_lines(pk128, pl) != 0) return -1;
+  uint8_t h[128];
+  bnc_hash_to_g1(m, n, h);
+  const fp hx = to_mont(from_be32(h + 1)), hy = to_mont(from_be32(h + 33));
+  fp xqh, yqh;
+  line_point(hx, hy, true, xqh, yqh);
+  g_cnt[0] = g_cnt[1] = 0;
+  fp xs, ys;
+  bool s_inf;
+  g1_decode(sig128, xs, ys, s_inf);
+  const int ok = bls_check(xs, ys, s_inf, xqh, yqh, false, gl, pl) ? 1 : 0;
+  out[0] = g_cnt[0];
+  out[1] = g_cnt[1];
+  return ok;
+}
+
 // e(P, Q) on the kernel's schedule, 12 canonical 32-byte big-endian values
 // in the order a.c0.a a.c0.b a.c1.a ... b.c2.b
 void bnc_pairing(const uint8_t* g1b, const uint8_t* g2b, uint8_t* out) {
