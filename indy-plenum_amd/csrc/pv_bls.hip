@@ -34,6 +34,12 @@ using namespace bn;
 constexpr int KEY_LINE_WORDS = N_LINES * LINE_WORDS;   // 2800 words per G2 point
 constexpr int MSG_WORDS = 4 * NL;                        // x_H, y_H, xq(-H), yq(-H)
 constexpr int BLS_BLOCK = 256;
+// waves per SIMD the check kernel is compiled for (-DPV_BLS_WAVES=1: 512
+// registers, every Fp12 temporary of the leaf functions in registers; 2: 256,
+// a little more stack)
+#ifndef PV_BLS_WAVES
+#define PV_BLS_WAVES 2
+#endif
 
 __device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
 #pragma unroll
@@ -106,7 +112,7 @@ __global__ void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, 
 
 // one lane per check, one key per wave (slots of `order` padded to 64 per key;
 // 0xffffffff = idle lane, which computes on the point at infinity and writes nothing)
-__global__ __launch_bounds__(BLS_BLOCK) void k_bls_verify(
+__global__ __launch_bounds__(BLS_BLOCK, PV_BLS_WAVES) void k_bls_verify(
     const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
     const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
     const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint8_t* __restrict__ verdict) {
