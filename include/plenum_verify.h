@@ -71,8 +71,9 @@ extern "C" {
 
 /* words per prepared key (pv_keys_prepare_device): an 8-way comb of -A —
  * affine multiples k * 2^(32 q) * (-A), k = 0..8, q = 0..7, 32 words each —
- * + status word (+ padding) */
-#define PV_KEY_WORDS 2312u
+ * + status word + padding to a multiple of 32 words (each key starts on a
+ * 128-byte line, so no 128-byte entry straddles two cache lines) */
+#define PV_KEY_WORDS 2336u
 
 /* Initialise the engine on the GPUs in device_mask (bit d = HIP device d;
  * 0 = all visible devices).  Idempotent.  Builds the base-point tables

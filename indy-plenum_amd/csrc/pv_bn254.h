@@ -332,26 +332,34 @@ PV_HD fp6 f6add(const fp6& x, const fp6& y) { return fp6{f2add(x.c0, y.c0), f2ad
 PV_HD fp6 f6sub(const fp6& x, const fp6& y) { return fp6{f2sub(x.c0, y.c0), f2sub(x.c1, y.c1), f2sub(x.c2, y.c2)}; }
 PV_HD fp6 f6neg(const fp6& x) { return fp6{f2neg(x.c0), f2neg(x.c1), f2neg(x.c2)}; }
 PV_HD fp6 f6mulv(const fp6& x) { return fp6{f2mulxi(x.c2), x.c0, x.c1}; }
-// Karatsuba over Fp2 (6 Fp2 products)
+// lazy Fp2 helpers (limbwise, no carry pass) for sums of normalised values
+// that are normalised once at the end: |limb| stays below 2^31
+PV_HD fp2 f2addL(const fp2& x, const fp2& y) { return fp2{add(x.a, y.a), add(x.b, y.b)}; }
+PV_HD fp2 f2subL(const fp2& x, const fp2& y) { return fp2{sub(x.a, y.a), sub(x.b, y.b)}; }
+PV_HD fp2 f2mulxiL(const fp2& x) { return fp2{sub(x.a, x.b), add(x.a, x.b)}; }
+PV_HD fp2 f2norm(const fp2& x) { return fp2{norm(x.a), norm(x.b)}; }
+
+// Karatsuba over Fp2 (6 Fp2 products); each output coefficient is one lazy
+// combination of normalised products (|limb| < 7 * 2^28) and one carry pass
 PV_BN_CALL fp6 f6mul(const fp6& a, const fp6& b) {
   const fp2 v0 = f2mul(a.c0, b.c0), v1 = f2mul(a.c1, b.c1), v2 = f2mul(a.c2, b.c2);
-  const fp2 s12 = f2mul(fp2{add(a.c1.a, a.c2.a), add(a.c1.b, a.c2.b)}, fp2{add(b.c1.a, b.c2.a), add(b.c1.b, b.c2.b)});
-  const fp2 s01 = f2mul(fp2{add(a.c0.a, a.c1.a), add(a.c0.b, a.c1.b)}, fp2{add(b.c0.a, b.c1.a), add(b.c0.b, b.c1.b)});
-  const fp2 s02 = f2mul(fp2{add(a.c0.a, a.c2.a), add(a.c0.b, a.c2.b)}, fp2{add(b.c0.a, b.c2.a), add(b.c0.b, b.c2.b)});
+  const fp2 s12 = f2mul(f2addL(a.c1, a.c2), f2addL(b.c1, b.c2));
+  const fp2 s01 = f2mul(f2addL(a.c0, a.c1), f2addL(b.c0, b.c1));
+  const fp2 s02 = f2mul(f2addL(a.c0, a.c2), f2addL(b.c0, b.c2));
   fp6 r;
-  r.c0 = f2add(f2mulxi(f2sub(f2sub(s12, v1), v2)), v0);
-  r.c1 = f2add(f2sub(f2sub(s01, v0), v1), f2mulxi(v2));
-  r.c2 = f2add(f2sub(f2sub(s02, v0), v2), v1);
+  r.c0 = f2norm(f2addL(f2mulxiL(f2subL(f2subL(s12, v1), v2)), v0));
+  r.c1 = f2norm(f2addL(f2subL(f2subL(s01, v0), v1), f2mulxiL(v2)));
+  r.c2 = f2norm(f2addL(f2subL(f2subL(s02, v0), v2), v1));
   return r;
 }
 // x * (b0 + b1 v): 5 Fp2 products
 PV_HD fp6 f6mul01(const fp6& x, const fp2& b0, const fp2& b1) {
   const fp2 t0 = f2mul(x.c0, b0), t1 = f2mul(x.c1, b1), t2 = f2mul(x.c2, b0), t3 = f2mul(x.c2, b1);
-  const fp2 m = f2mul(fp2{add(x.c0.a, x.c1.a), add(x.c0.b, x.c1.b)}, fp2{add(b0.a, b1.a), add(b0.b, b1.b)});
+  const fp2 m = f2mul(f2addL(x.c0, x.c1), f2addL(b0, b1));
   fp6 r;
-  r.c0 = f2add(t0, f2mulxi(t3));
-  r.c1 = f2sub(f2sub(m, t0), t1);
-  r.c2 = f2add(t1, t2);
+  r.c0 = f2norm(f2addL(t0, f2mulxiL(t3)));
+  r.c1 = f2norm(f2subL(f2subL(m, t0), t1));
+  r.c2 = f2norm(f2addL(t1, t2));
   return r;
 }
 PV_BN_CALL fp6 f6inv(const fp6& x) {
@@ -368,12 +376,24 @@ PV_HD fp12 f12conj(const fp12& x) { return fp12{x.a, f6neg(x.b)}; }
 PV_BN_CALL fp12 f12mul(const fp12& x, const fp12& y) {   // Karatsuba: 3 Fp6 products
   const fp6 t0 = f6mul(x.a, y.a), t1 = f6mul(x.b, y.b);
   const fp6 s = f6mul(f6add(x.a, x.b), f6add(y.a, y.b));
-  return fp12{f6add(t0, f6mulv(t1)), f6sub(f6sub(s, t0), t1)};
+  fp12 r;
+  r.a.c0 = f2norm(f2addL(t0.c0, f2mulxiL(t1.c2)));
+  r.a.c1 = f2norm(f2addL(t0.c1, t1.c0));
+  r.a.c2 = f2norm(f2addL(t0.c2, t1.c1));
+  r.b.c0 = f2norm(f2subL(f2subL(s.c0, t0.c0), t1.c0));
+  r.b.c1 = f2norm(f2subL(f2subL(s.c1, t0.c1), t1.c1));
+  r.b.c2 = f2norm(f2subL(f2subL(s.c2, t0.c2), t1.c2));
+  return r;
 }
 PV_BN_CALL fp12 f12sqr(const fp12& x) {   // complex squaring: 2 Fp6 products
   const fp6 t = f6mul(x.a, x.b);
   const fp6 s = f6mul(f6add(x.a, x.b), f6add(x.a, f6mulv(x.b)));
-  return fp12{f6sub(f6sub(s, t), f6mulv(t)), f6add(t, t)};
+  fp12 r;   // (s - t - v t) + 2t w
+  r.a.c0 = f2norm(f2subL(f2subL(s.c0, t.c0), f2mulxiL(t.c2)));
+  r.a.c1 = f2norm(f2subL(f2subL(s.c1, t.c1), t.c0));
+  r.a.c2 = f2norm(f2subL(f2subL(s.c2, t.c2), t.c1));
+  r.b = fp6{f2dbl(t.c0), f2dbl(t.c1), f2dbl(t.c2)};
+  return r;
 }
 PV_BN_CALL fp12 f12inv(const fp12& x) {
   const fp6 d = f6inv(f6sub(f6mul(x.a, x.a), f6mulv(f6mul(x.b, x.b))));
@@ -383,7 +403,12 @@ PV_BN_CALL fp12 f12inv(const fp12& x) {
 PV_BN_CALL fp12 f12mul_line(const fp12& f, const fp2& b0, const fp2& b1) {
   const fp6 t = f6mul01(f.b, b0, b1);
   const fp6 s = f6mul01(f.a, b0, b1);
-  return fp12{f6add(f.a, f6mulv(t)), f6add(f.b, s)};
+  fp12 r;   // (f.a + v t) + (f.b + s) w, one carry pass per coefficient
+  r.a.c0 = f2norm(f2addL(f.a.c0, f2mulxiL(t.c2)));
+  r.a.c1 = f2norm(f2addL(f.a.c1, t.c0));
+  r.a.c2 = f2norm(f2addL(f.a.c2, t.c1));
+  r.b = f6add(f.b, s);
+  return r;
 }
 PV_HD bool f12is_one(const fp12& x) {
   bool ok = eq(x.a.c0.a, fone()) && is_zero(x.a.c0.b);

@@ -594,7 +594,7 @@ constexpr int BW_CHUNKS = 8;
 constexpr int KT_ENTRY = 32;
 constexpr int KT_TABLE = 9 * KT_ENTRY;
 constexpr int KEY_STATUS = COMB_Q * KT_TABLE;
-constexpr int KEY_WORDS = KEY_STATUS + 8;
+constexpr int KEY_WORDS = KEY_STATUS + 32;   // status word + padding: every key starts on a 128-byte line
 constexpr int KEY_SCRATCH = 8 * COMB_Q * 10;   // prefix products of the shared inversion
 
 PV_HD void store_xyz(uint32_t* p, const ge_p3& q) {

@@ -241,7 +241,7 @@ def pack_messages(msgs):
 
 
 PV_FLAG_DEDUP_KEYS = 1
-PV_KEY_WORDS = 2312
+PV_KEY_WORDS = 2336
 
 
 def verify_batch_arrays(pk, sig, blob, off, device_mask=0, dedup_keys=True):
