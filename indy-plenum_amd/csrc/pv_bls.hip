@@ -27,18 +27,19 @@
 #include "pv_bn254.h"
 #include "pv_sha256.h"
 
-namespace {
+// a named namespace: profilers show the kernels as pvbls::k_bls_*
+namespace pvbls {
 
 using namespace bn;
 
 constexpr int KEY_LINE_WORDS = N_LINES * LINE_WORDS;   // 2800 words per G2 point
 constexpr int MSG_WORDS = 4 * NL;                        // x_H, y_H, xq(-H), yq(-H)
 constexpr int BLS_BLOCK = 256;
-// waves per SIMD the check kernel is compiled for (-DPV_BLS_WAVES=1: 512
-// registers, every Fp12 temporary of the leaf functions in registers; 2: 256,
-// a little more stack)
+// waves per SIMD the check kernel is compiled for: 1 (512 registers) measured
+// 1.77x the throughput of 2 (256 registers, the tower temporaries spill) on the
+// full C3-BLS batch (profiles/r03_ab_bls_waves.jsonl)
 #ifndef PV_BLS_WAVES
-#define PV_BLS_WAVES 2
+#define PV_BLS_WAVES 1
 #endif
 
 __device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
@@ -302,7 +303,9 @@ int collect_times(BlsDev& d) {
   return PV_OK;
 }
 
-}  // namespace
+}  // namespace pvbls
+
+using namespace pvbls;
 
 extern "C" {
 

@@ -341,7 +341,7 @@ PV_HD fp2 f2norm(const fp2& x) { return fp2{norm(x.a), norm(x.b)}; }
 
 // Karatsuba over Fp2 (6 Fp2 products); each output coefficient is one lazy
 // combination of normalised products (|limb| < 7 * 2^28) and one carry pass
-PV_BN_CALL fp6 f6mul(const fp6& a, const fp6& b) {
+PV_HD fp6 f6mul_i(const fp6& a, const fp6& b) {
   const fp2 v0 = f2mul(a.c0, b.c0), v1 = f2mul(a.c1, b.c1), v2 = f2mul(a.c2, b.c2);
   const fp2 s12 = f2mul(f2addL(a.c1, a.c2), f2addL(b.c1, b.c2));
   const fp2 s01 = f2mul(f2addL(a.c0, a.c1), f2addL(b.c0, b.c1));
@@ -352,6 +352,7 @@ PV_BN_CALL fp6 f6mul(const fp6& a, const fp6& b) {
   r.c2 = f2norm(f2addL(f2subL(f2subL(s02, v0), v2), v1));
   return r;
 }
+PV_BN_CALL fp6 f6mul(const fp6& a, const fp6& b) { return f6mul_i(a, b); }
 // x * (b0 + b1 v): 5 Fp2 products
 PV_HD fp6 f6mul01(const fp6& x, const fp2& b0, const fp2& b1) {
   const fp2 t0 = f2mul(x.c0, b0), t1 = f2mul(x.c1, b1), t2 = f2mul(x.c2, b0), t3 = f2mul(x.c2, b1);
@@ -385,9 +386,9 @@ PV_BN_CALL fp12 f12mul(const fp12& x, const fp12& y) {   // Karatsuba: 3 Fp6 pro
   r.b.c2 = f2norm(f2subL(f2subL(s.c2, t0.c2), t1.c2));
   return r;
 }
-PV_BN_CALL fp12 f12sqr(const fp12& x) {   // complex squaring: 2 Fp6 products
-  const fp6 t = f6mul(x.a, x.b);
-  const fp6 s = f6mul(f6add(x.a, x.b), f6add(x.a, f6mulv(x.b)));
+PV_HD fp12 f12sqr_i(const fp12& x) {   // complex squaring: 2 Fp6 products
+  const fp6 t = f6mul_i(x.a, x.b);
+  const fp6 s = f6mul_i(f6add(x.a, x.b), f6add(x.a, f6mulv(x.b)));
   fp12 r;   // (s - t - v t) + 2t w
   r.a.c0 = f2norm(f2subL(f2subL(s.c0, t.c0), f2mulxiL(t.c2)));
   r.a.c1 = f2norm(f2subL(f2subL(s.c1, t.c1), t.c0));
@@ -395,12 +396,13 @@ PV_BN_CALL fp12 f12sqr(const fp12& x) {   // complex squaring: 2 Fp6 products
   r.b = fp6{f2dbl(t.c0), f2dbl(t.c1), f2dbl(t.c2)};
   return r;
 }
+PV_BN_CALL fp12 f12sqr(const fp12& x) { return f12sqr_i(x); }
 PV_BN_CALL fp12 f12inv(const fp12& x) {
   const fp6 d = f6inv(f6sub(f6mul(x.a, x.a), f6mulv(f6mul(x.b, x.b))));
   return fp12{f6mul(x.a, d), f6neg(f6mul(x.b, d))};
 }
 // f * (1 + (b0 + b1 v) w): the normalised line (5 + 5 Fp2 products)
-PV_BN_CALL fp12 f12mul_line(const fp12& f, const fp2& b0, const fp2& b1) {
+PV_HD fp12 f12mul_line_i(const fp12& f, const fp2& b0, const fp2& b1) {
   const fp6 t = f6mul01(f.b, b0, b1);
   const fp6 s = f6mul01(f.a, b0, b1);
   fp12 r;   // (f.a + v t) + (f.b + s) w, one carry pass per coefficient
@@ -410,6 +412,7 @@ PV_BN_CALL fp12 f12mul_line(const fp12& f, const fp2& b0, const fp2& b1) {
   r.b = f6add(f.b, s);
   return r;
 }
+PV_BN_CALL fp12 f12mul_line(const fp12& f, const fp2& b0, const fp2& b1) { return f12mul_line_i(f, b0, b1); }
 PV_HD bool f12is_one(const fp12& x) {
   bool ok = eq(x.a.c0.a, fone()) && is_zero(x.a.c0.b);
   ok = ok && f2is_zero(x.a.c1) && f2is_zero(x.a.c2);
@@ -471,7 +474,7 @@ PV_HD fp2 three_plus_two(const fp2& t, const fp2& z) {    // 3t + 2z
   const fp2 d = f2add(t, z);
   return f2add(f2dbl(d), t);
 }
-PV_BN_CALL fp12 cyc_sqr(const fp12& x) {
+PV_HD fp12 cyc_sqr_i(const fp12& x) {
   fp2 t0, t1, t2, t3, t4, t5;
   fp4_sqr(t0, t1, x.a.c0, x.b.c1);
   fp4_sqr(t2, t3, x.b.c0, x.a.c2);
@@ -485,6 +488,7 @@ PV_BN_CALL fp12 cyc_sqr(const fp12& x) {
   r.b.c2 = three_plus_two(t3, x.b.c2);
   return r;
 }
+PV_BN_CALL fp12 cyc_sqr(const fp12& x) { return cyc_sqr_i(x); }
 // x^u (u = -0x4080000000000001) in the cyclotomic subgroup: x^(2^62 + 2^55 + 1), conjugated
 // (the squarings' 3t -/+ 2z feed the input back unreduced: values double per
 // squaring, so every fourth one is followed by a reduction)
@@ -493,12 +497,12 @@ PV_BN_CALL fp12 f12reduce(const fp12& x) { return fp12{f6reduce(x.a), f6reduce(x
 PV_BN_CALL fp12 cyc_pow_u(const fp12& x) {
   fp12 t = x;
   for (int i = 0; i < 7; ++i) {
-    t = cyc_sqr(t);
+    t = cyc_sqr_i(t);
     if ((i & 3) == 3) t = f12reduce(t);
   }
   t = f12mul(t, x);                  // x^(2^7 + 1)
   for (int i = 0; i < 55; ++i) {
-    t = cyc_sqr(t);
+    t = cyc_sqr_i(t);
     if ((i & 3) == 3) t = f12reduce(t);
   }
   t = f12mul(t, x);                  // x^(2^62 + 2^55 + 1)
@@ -614,6 +618,31 @@ PV_HD fp12 miller_fixed(const uint32_t* const lines[T_], const fp* xq, const fp*
       f = f12mul_line(f, f2mulfp(ld_f2(L), xq[t]), f2mulfp(ld_f2(L + 2 * NL), yq[t]));
     }
   }
+  return f;
+}
+
+// the kernel's Miller product of two pairings: ONE out-of-line function whose
+// loop body (squaring + the two lines) is inlined, so f stays in registers
+// across the 68 steps (as calls, f went through the stack at every one)
+PV_HD fp12 line2_i(const fp12& f, const uint32_t* Lg, const uint32_t* Lp, const fp* xq, const fp* yq) {
+  fp12 r = f12mul_line_i(f, f2mulfp(ld_f2(Lg), xq[0]), f2mulfp(ld_f2(Lg + 2 * NL), yq[0]));
+  return f12mul_line_i(r, f2mulfp(ld_f2(Lp), xq[1]), f2mulfp(ld_f2(Lp + 2 * NL), yq[1]));
+}
+PV_BN_CALL fp12 miller2(const uint32_t* g_lines, const uint32_t* pk_lines, const fp* xq, const fp* yq) {
+  fp12 f = f12one();
+  int k = 0;
+  // steps: bit i = 63..0 doubling (squaring first, except for f = 1), then an
+  // addition step for the set bits; 2 Frobenius steps after the conjugation
+  for (int i = 63; i >= 0; --i) {
+    for (int add = 0; add < 2; ++add) {
+      if (add && !ate_bit(i)) break;
+      if (!add && i != 63) f = f12sqr_i(f);
+      f = line2_i(f, g_lines + LINE_WORDS * k, pk_lines + LINE_WORDS * k, xq, yq);
+      ++k;
+    }
+  }
+  f = f12conj(f);
+  for (int j = 0; j < 2; ++j, ++k) f = line2_i(f, g_lines + LINE_WORDS * k, pk_lines + LINE_WORDS * k, xq, yq);
   return f;
 }
 
@@ -778,8 +807,7 @@ PV_HD bool bls_check(const fp& xs, const fp& ys, bool s_inf, const fp& xqh, cons
   }
   xq[1] = xqh;
   yq[1] = yqh;
-  const uint32_t* L[2] = {g_lines, pk_lines};
-  const fp12 f = final_exp(miller_fixed<2>(L, xq, yq));
+  const fp12 f = final_exp(miller2(g_lines, pk_lines, xq, yq));
   if (s_inf || pk_inf) return s_inf && pk_inf;
   return f12is_one(f);
 }
