@@ -928,7 +928,7 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   if (keyed) {
     HIP_OK(d.ktab.ensure(nk * pv::KEYTAB_WORDS));
     HIP_OK(d.kidx.ensure(m));
-    HIP_OK(d.kscr.ensure(nk * pv::KEYTAB_SCRATCH));
+    HIP_OK(d.kscr.ensure((nk + 63) / 64 * 64 * pv::KEYTAB_SCRATCH));   // lane-interleaved per 64 keys
     HIP_OK(hipMemcpyAsync(d.pk.p, upk.data(), nk * 32, hipMemcpyHostToDevice, d.copy));
     HIP_OK(hipMemcpyAsync(d.kidx.p, idx.data(), m * 4, hipMemcpyHostToDevice, d.copy));
     HIP_OK(hipEventRecord(d.copied, d.copy));
@@ -1208,7 +1208,7 @@ int pv_keys_prepare_device_async(const uint8_t* pk, uint64_t k, uint32_t* ktab, 
   int rc = ws_begin(d->ws[slot], s);
   if (rc) return rc;
   DevBuf<uint32_t>& scr = slot ? d->kscr2 : d->kscr;
-  HIP_OK(scr.ensure(k * pv::KEYTAB_SCRATCH));
+  HIP_OK(scr.ensure((k + 63) / 64 * 64 * pv::KEYTAB_SCRATCH));
   HIP_OK(pv::launch_keys(pk, k, ktab, scr.p, s));
   return ws_end(d->ws[slot], s);
 }
@@ -1224,7 +1224,7 @@ int pv_keys_prepare_device(const uint8_t* pk, uint64_t k, uint32_t* ktab, int de
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
   int rc = ws_begin(d->ws[0], s);
   if (rc) return rc;
-  HIP_OK(d->kscr.ensure(k * pv::KEYTAB_SCRATCH));
+  HIP_OK(d->kscr.ensure((k + 63) / 64 * 64 * pv::KEYTAB_SCRATCH));
   HIP_OK(pv::launch_keys(pk, k, ktab, d->kscr.p, s));
   rc = ws_end(d->ws[0], s);
   if (rc) return rc;

@@ -103,7 +103,7 @@ hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32
 // prepared keys: KEYTAB_WORDS words per key (8 comb tables of affine multiples
 // k * 2^(32 q) * (-A) + status); KEYTAB_SCRATCH words of scratch per key
 constexpr int KEYTAB_WORDS = 8 * 9 * 32 + 32;
-constexpr int KEYTAB_SCRATCH = 64 * 10;
+constexpr int KEYTAB_SCRATCH = 64 * 40;   // projective entries + prefix products (lane-interleaved per 64 keys)
 hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
 
 // keygen + sign: pk[i], sig[i] for seed[i] over M_i

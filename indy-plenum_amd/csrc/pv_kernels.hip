@@ -837,7 +837,8 @@ hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32
 __global__ __launch_bounds__(256, PV_KEYS_WAVES) void k_keys(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
                                                uint32_t* __restrict__ scr) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j < k) key_prepare(ktab + j * KEY_WORDS, scr + j * KEY_SCRATCH, pk + 32 * j);
+  // scratch lane-interleaved per wave: word w of key j at [(j / 64) * KEY_SCRATCH + w] * 64 + j % 64
+  if (j < k) key_prepare<64>(ktab + j * KEY_WORDS, scr + (j / 64) * (uint64_t)(KEY_SCRATCH * 64) + j % 64, pk + 32 * j);
 }
 
 hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s) {

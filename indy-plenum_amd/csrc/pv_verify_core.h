@@ -595,7 +595,14 @@ constexpr int KT_ENTRY = 32;
 constexpr int KT_TABLE = 9 * KT_ENTRY;
 constexpr int KEY_STATUS = COMB_Q * KT_TABLE;
 constexpr int KEY_WORDS = KEY_STATUS + 32;   // status word + padding: every key starts on a 128-byte line
-constexpr int KEY_SCRATCH = 8 * COMB_Q * 10;   // prefix products of the shared inversion
+// per-key scratch: the projective entries (X, Y, Z of the 8 * COMB_Q multiples)
+// and the prefix products of their shared inversion.  Private to key_prepare,
+// so k_keys lays it out lane-interleaved ([word][lane] per 64 keys: every
+// scratch load and store of a wave is one contiguous 256-byte row); only the
+// final affine entries go to the key-major table the curve kernel reads.
+constexpr int KS_XYZ = 0;
+constexpr int KS_PREFIX = 8 * COMB_Q * 30;
+constexpr int KEY_SCRATCH = KS_PREFIX + 8 * COMB_Q * 10;
 
 PV_HD void store_xyz(uint32_t* p, const ge_p3& q) {
   store_fe(p, q.X);
@@ -603,7 +610,9 @@ PV_HD void store_xyz(uint32_t* p, const ge_p3& q) {
   store_fe(p + 20, q.Z);
 }
 
-// kt: KEY_WORDS words; scr: KEY_SCRATCH words of per-key scratch
+// kt: KEY_WORDS words (key-major); scr: KEY_SCRATCH words of this key's
+// scratch, word w at scr[w * LS] (LS = 64 on the device: lane-interleaved)
+template <int LS = 1>
 PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
   uint32_t A[8];
   load8(A, pk);
@@ -613,28 +622,34 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
   // words after the status are padding)
   kt[KEY_STATUS] = ok ? 1u : 0u;
   if (!ok) return;
-  // projective multiples k * A_q (X, Y, Z) into the entry slots
+  // projective multiples k * A_q (X, Y, Z) into the scratch, entry e = 8 q + k - 1
+  auto xyz = [&](int e) { return scr + (KS_XYZ + 30 * e) * LS; };
+  auto pre = [&](int e) { return scr + (KS_PREFIX + 10 * e) * LS; };
   fe zacc;
 #pragma unroll 1
   for (int q = 0; q < COMB_Q; ++q) {
-    uint32_t* tq = kt + q * KT_TABLE;
     ge_cached c1;
     ge_p3_to_cached(c1, P);
     ge_p3 Q = P;
-    store_xyz(tq + KT_ENTRY, Q);
+    store_fe<LS>(xyz(8 * q), Q.X);
+    store_fe<LS>(xyz(8 * q) + 10 * LS, Q.Y);
+    store_fe<LS>(xyz(8 * q) + 20 * LS, Q.Z);
     // prefix products of the Z's for the shared inversion, formed while each
-    // Z is in registers (entry e = 8 q + k - 1)
+    // Z is in registers
     if (q == 0) fe_copy(zacc, Q.Z);
     else fe_mul(zacc, zacc, Q.Z);
-    store_fe(scr + 10 * (8 * q), zacc);
+    store_fe<LS>(pre(8 * q), zacc);
 #pragma unroll 1
     for (int k = 2; k <= 8; ++k) {
       ge_p1p1 t;
       ge_add_cached(t, Q, c1, false);
       ge_p1p1_to_p3(Q, t);
-      store_xyz(tq + k * KT_ENTRY, Q);
+      const int e = 8 * q + k - 1;
+      store_fe<LS>(xyz(e), Q.X);
+      store_fe<LS>(xyz(e) + 10 * LS, Q.Y);
+      store_fe<LS>(xyz(e) + 20 * LS, Q.Z);
       fe_mul(zacc, zacc, Q.Z);
-      store_fe(scr + 10 * (8 * q + k - 1), zacc);
+      store_fe<LS>(pre(e), zacc);
     }
     if (q + 1 < COMB_Q) {  // A_{q+1} = 2^32 A_q = 2^29 (8 A_q)
       ge_p1p1 t;
@@ -659,13 +674,10 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
   fe_invert(acc, zacc);
   fe d2;
   fe_const_d2(d2);
-  {
-    const uint32_t* slot = kt + ((NE - 1) >> 3) * KT_TABLE + (((NE - 1) & 7) + 1) * KT_ENTRY;
-    load_fe(un, scr + 10 * (NE - 2));
-    load_fe(zn, slot + 20);
-    load_fe(xn, slot);
-    load_fe(yn, slot + 10);
-  }
+  load_fe<LS>(un, pre(NE - 2));
+  load_fe<LS>(xn, xyz(NE - 1));
+  load_fe<LS>(yn, xyz(NE - 1) + 10 * LS);
+  load_fe<LS>(zn, xyz(NE - 1) + 20 * LS);
 #pragma unroll 1
   for (int e = NE - 1; e >= 0; --e) {
     uint32_t* slot = kt + (e >> 3) * KT_TABLE + ((e & 7) + 1) * KT_ENTRY;
@@ -674,11 +686,10 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
     fe_copy(x, xn);
     fe_copy(y, yn);
     if (e > 0) {
-      const uint32_t* nslot = kt + ((e - 1) >> 3) * KT_TABLE + (((e - 1) & 7) + 1) * KT_ENTRY;
-      if (e > 1) load_fe(un, scr + 10 * (e - 2));
-      load_fe(zn, nslot + 20);
-      load_fe(xn, nslot);
-      load_fe(yn, nslot + 10);
+      if (e > 1) load_fe<LS>(un, pre(e - 2));
+      load_fe<LS>(xn, xyz(e - 1));
+      load_fe<LS>(yn, xyz(e - 1) + 10 * LS);
+      load_fe<LS>(zn, xyz(e - 1) + 20 * LS);
     }
     fe zi;
     if (e > 0) {
