@@ -340,24 +340,38 @@ def end_to_end(batch, dedup, reps=5):
 def small_batch_latency(batch, sizes=(1, 100, 1000), reps=20):
     """Host-buffer call time of Plenum's per-pass batch sizes (stp_core/config.py:32-33:
     <= 100 client / 1,000 node messages) on this rank's first signatures: the
-    one-launch latency kernel.  Median and min of `reps` calls."""
+    one-launch latency kernel, with the keys uncached (top level)
+    and in the persistent device key cache ('cached': the keyed latency kernel,
+    DESIGN.md 4f).  Median and min of `reps` calls."""
     pk, sig = batch.pk.cpu().numpy(), batch.sig.cpu().numpy()
     off = batch.off.cpu().numpy().astype(np.uint64)
     blob = batch.blob.cpu().numpy()
     want = ~batch.tamper.cpu().numpy().astype(bool)
-    out, mism = {}, 0
-    for n in sizes:
-        args = (pk[:n], sig[:n], blob[:int(off[n])], off[:n + 1])
-        got = nat.verify_batch_arrays(*args, device_mask=1 << batch.device.index)
-        mism += int((got != want[:n]).sum())
-        ts = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            nat.verify_batch_arrays(*args, device_mask=1 << batch.device.index)
-            ts.append(time.perf_counter() - t0)
-        ts.sort()
-        out[str(n)] = {'ms_median': round(ts[reps // 2] * 1e3, 3), 'ms_min': round(ts[0] * 1e3, 3)}
-    out['verdict_mismatches'] = mism
+    mask = 1 << batch.device.index
+
+    def measure():
+        res, bad = {}, 0
+        for n in sizes:
+            args = (pk[:n], sig[:n], blob[:int(off[n])], off[:n + 1])
+            got = nat.verify_batch_arrays(*args, device_mask=mask)
+            bad += int((got != want[:n]).sum())
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                nat.verify_batch_arrays(*args, device_mask=mask)
+                ts.append(time.perf_counter() - t0)
+            ts.sort()
+            res[str(n)] = {'ms_median': round(ts[reps // 2] * 1e3, 3), 'ms_min': round(ts[0] * 1e3, 3)}
+        return res, bad
+
+    nat.keycache_clear()
+    out, mism = measure()
+    nat.keycache_add(pk[:max(sizes)])
+    try:
+        out['cached'], m2 = measure()
+    finally:
+        nat.keycache_clear()
+    out['verdict_mismatches'] = mism + m2
     return out
 
 

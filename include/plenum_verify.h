@@ -145,6 +145,23 @@ int pv_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, const 
                            const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n, uint8_t *verdict,
                            uint64_t *bitmap, int device, void *stream);
 
+/* Persistent verifying-key cache of host-buffer calls.  pv_keycache_add
+ * prepares the comb tables of the k 32-byte keys in pk on every initialised
+ * device (and on devices initialised later) and keeps them until
+ * pv_keycache_clear / pv_shutdown; keys already cached are skipped.  A
+ * pv_verify_batch shard of a Looper-pass size (<= the latency size) then looks
+ * up every signature's key on the host: signatures under cached keys run the
+ * keyed latency kernel (no decompression of A; the hashed key bytes are still
+ * the caller's), the rest the generic one, in the same call.  Verdicts are
+ * identical with or without the cache -- a key libsodium refuses is cached as
+ * refused.  Fill it from the keys a node already knows: node keys, the client
+ * DIDs of SimpleAuthNr.addIdr / getVerkey's NYM state lookups
+ * (plenum/server/client_authn.py:145-168), replacing the per-call VerifyKey(key) of
+ * stp_core/crypto/nacl_wrappers.py:71-81.  At most 2^32 - 2 keys. */
+int pv_keycache_add(const uint8_t *pk, uint64_t k);
+int pv_keycache_clear(void);
+int pv_keycache_size(uint64_t *count);
+
 /* SHA-256 / Merkle tree hashing.
  *   pv_sha256_batch[_device]  digests[i] (32 bytes) = SHA-256(prefix || M_i); prefix -1 = none,
  *                             0..255 = that single byte.  Replaces the per-request
@@ -272,6 +289,13 @@ int pv_set_curve_mode(uint32_t mode);
  * identical.  Default 32768 (the measured crossover with the throughput path
  * is between 32k and 64k signatures), env PV_LAT_MAX at pv_init; 0 disables. */
 int pv_set_lat_max(uint64_t max_signatures);
+/* Keyed batches (prepared keys: pv_verify_keyed_device, the key cache below)
+ * of at most max_signatures signatures run the keyed latency kernel: the comb
+ * of the prepared key split over two lane quads per signature (28 doublings
+ * and 40 affine adds per lane) while one lane per signature hashes, -R decoded
+ * beside the hash, one launch.  Verdicts are identical.  Default 8192, env
+ * PV_LAT_KEYED_MAX at pv_init; 0 disables (the keyed throughput kernel). */
+int pv_set_lat_keyed_max(uint64_t max_signatures);
 /* Latency kernel: PV_LAT_QUAD (default, lane quads per point) or PV_LAT_PAIR
  * (the previous lane-pair kernel, one lane per point; A/B).  Env
  * PV_LAT_KERNEL=quad|pair at pv_init. */

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <condition_variable>
 #include <memory>
+#include <random>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -53,6 +54,9 @@ int fail(int code, const char* fmt, ...) {
 // generic batches of at most this many signatures run the latency-mode curve
 // kernel (k_verify_quad: one launch, lane quads per point); PV_LAT_MAX env overrides (0 disables)
 #define PV_LAT_MAX 32768
+// keyed batches (prepared keys) of at most this many signatures run the keyed
+// latency kernel (k_verify_quad_keyed); PV_LAT_KEYED_MAX env overrides (0 disables)
+#define PV_LAT_KEYED_MAX 8192
 // shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
 #define PV_DEDUP_SAMPLE_MIN 262144
 // chunk gathers into the pinned staging ring use up to this many host threads
@@ -272,6 +276,61 @@ struct KeyIndex {
   }
 };
 
+// Persistent verifying-key cache (pv_keycache_add): host-side index of the
+// cached 32-byte keys; key j's comb tables sit in slot j of every device's
+// `kc` table.  Open addressing over all 32 bytes with a per-process random
+// seed (keys come from the ledger, so their first bytes are attacker-chosen).
+struct KeyCache {
+  std::vector<uint8_t> keys;      // 32 bytes per cached key, slot order
+  std::vector<uint32_t> slot;     // 0 = empty, else 1 + slot
+  uint64_t mask = 0;
+  uint64_t seed = 0;
+  uint64_t count() const { return keys.size() / 32; }
+  uint64_t hash(const uint8_t* k) const {
+    uint64_t h = seed;
+    for (int i = 0; i < 4; ++i) {
+      uint64_t w;
+      memcpy(&w, k + 8 * i, 8);
+      h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+      h ^= h >> 29;
+    }
+    return h;
+  }
+  // slot of key k, or UINT32_MAX
+  uint32_t find(const uint8_t* k) const {
+    if (slot.empty()) return UINT32_MAX;
+    for (uint64_t p = hash(k) & mask;; p = (p + 1) & mask) {
+      const uint32_t v = slot[p];
+      if (!v) return UINT32_MAX;
+      if (!memcmp(keys.data() + 32 * (uint64_t)(v - 1), k, 32)) return v - 1;
+    }
+  }
+  void rehash(uint64_t cap) {
+    slot.assign(cap, 0);
+    mask = cap - 1;
+    for (uint64_t j = 0; j < count(); ++j)
+      for (uint64_t p = hash(keys.data() + 32 * j) & mask;; p = (p + 1) & mask)
+        if (!slot[p]) {
+          slot[p] = (uint32_t)(j + 1);
+          break;
+        }
+  }
+  // append keys (already known to be absent and distinct) as new slots
+  void commit(const std::vector<uint8_t>& add) {
+    if (!seed) seed = ((uint64_t)std::random_device{}() << 32 | std::random_device{}()) | 1;
+    keys.insert(keys.end(), add.begin(), add.end());
+    uint64_t cap = slot.size() ? slot.size() : 64;
+    while (cap < 2 * count()) cap <<= 1;
+    rehash(cap);
+  }
+  void clear() {
+    keys.clear();
+    slot.clear();
+    mask = 0;
+  }
+};
+KeyCache g_kc;
+
 // PV_CURVE_MODE (read at pv_init): "half" (default) = half-size scalars with
 // full-length tasks for deferred records; "full" = every record deferred
 // (full-length verdicts through the same kernel: A/B timing and tests);
@@ -341,6 +400,7 @@ struct Device {
   uint64_t ramp = PV_HOST_RAMP;
   size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
   uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; PV_LAT_MAX env (0 = off)
+  uint64_t lat_keyed_max = PV_LAT_KEYED_MAX;  // keyed batches up to this size: k_verify_quad_keyed
   bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
   // host-buffer chunks of generic batches: one k_chunk_half launch per chunk
   // + one k_verify_quad_list pass for the deferred records; PV_HOST_FUSED=0:
@@ -374,6 +434,9 @@ struct Device {
   DevBuf<uint32_t> ktab, kidx;  // prepared keys + per-signature key index (deduplicated host batches)
   DevBuf<uint32_t> kscr, kscr2;  // key-preparation scratch (kscr2: async slot 1)
   DevBuf<uint32_t> mk0, mk1;    // Merkle level ping-pong / leaf digests
+  DevBuf<uint32_t> kc;          // persistent key cache: slot j = comb tables of g_kc key j
+  uint64_t kc_count = 0;        // slots prepared on this device
+  DevBuf<uint8_t> kcpk;         // staging of keys being added
   int sha256_blocks = 0;
   int curve_blocks_keyed = 0;
   int curve_half_blocks = 0;
@@ -444,6 +507,11 @@ int init_device(Device& d) {
     const long v = atol(t);
     if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_MAX must be in 0..1048576 (got %s)", t);
     d.lat_max = (uint64_t)v;
+  }
+  if (const char* t = getenv("PV_LAT_KEYED_MAX")) {
+    const long v = atol(t);
+    if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_KEYED_MAX must be in 0..1048576 (got %s)", t);
+    d.lat_keyed_max = (uint64_t)v;
   }
   if (const char* t = getenv("PV_HOST_FUSED")) {
     if (strcmp(t, "0") != 0 && strcmp(t, "1") != 0) return fail(PV_EINVAL, "PV_HOST_FUSED must be 0 or 1 (got %s)", t);
@@ -525,6 +593,8 @@ void release_device(Device& d) {
   d.off.release(); d.batch_off.release();
   d.sender.release(); d.votes.release(); d.reached.release(); d.scan.release(); d.tflag.release(); d.tbits.release();
   d.ktab.release(); d.kidx.release(); d.kscr.release(); d.kscr2.release(); d.mk0.release(); d.mk1.release();
+  d.kc.release(); d.kcpk.release();
+  d.kc_count = 0;
   for (auto& e : d.ev)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   for (auto& r : d.live_pool)
@@ -584,10 +654,15 @@ uint64_t* stage_bitmap(Workspace& w, uint64_t* bitmap, uint64_t n, int& rc) {
 bool lat_fused(const Device& d, const uint32_t* ktab, uint64_t n) {
   return !ktab && d.mode != CurveMode::Grouped && n <= d.lat_max && d.lat_quad;
 }
+// small keyed batches: one k_verify_quad_keyed launch
+bool lat_keyed(const Device& d, const uint32_t* ktab, uint64_t n) {
+  return ktab && n <= d.lat_keyed_max && d.lat_quad;
+}
 
 int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                  const uint64_t* off, uint64_t n, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
                  const uint32_t* kidx) {
+  if (lat_keyed(d, ktab, n)) return PV_OK;   // k_verify_quad_keyed runs the whole verify
   if (lat_fused(d, ktab, n)) {
     // k_verify_quad runs the whole verify; only the deferred counter is reset
     HIP_OK(w.qc.ensure(2));
@@ -618,7 +693,11 @@ int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig
                   const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
                   const uint32_t* kidx) {
   const bool half = !ktab && d.mode != CurveMode::Grouped;
-  if (lat_fused(d, ktab, n)) {
+  if (lat_keyed(d, ktab, n)) {
+    // small keyed batch: one launch, the comb split over the signature's two
+    // lane quads (the hashed key bytes are pk[kidx[i]])
+    HIP_OK(pv::launch_verify_quad_keyed(pk, true, sig, blob, off, n, nullptr, ktab, kidx, d.bw.p, verdict, bm, s));
+  } else if (lat_fused(d, ktab, n)) {
     // small batch: one launch, 8 lanes per signature (each point on a lane
     // quad) plus one hashing lane per signature in a second wave
     HIP_OK(pv::launch_verify_quad(pk, sig, blob, off, n, d.bw.p, verdict, bm, w.qc.p, d.mode == CurveMode::Full, s));
@@ -741,7 +820,8 @@ bool host_locked(const void* p, size_t n) {
 
 uint64_t small_bytes(const HostBatch& hb, uint64_t s, uint64_t e) {
   const uint64_t m = e - s;
-  return (m + 1) * 8 + m * 96 + (hb.off[e] - hb.off[s]) + 16;
+  // + the key-cache tail: 8-byte alignment, list count, kidx and the two lists
+  return (m + 1) * 8 + m * 96 + (hb.off[e] - hb.off[s]) + 16 + 16 + 8 * m;
 }
 
 int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
@@ -773,11 +853,45 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   if (bad.load())
     return fail(PV_EINVAL, "msg_off not monotone in [%llu, %llu]", (unsigned long long)s, (unsigned long long)e);
   memset(base + o_blob + bytes, 0, 16);   // the hash reads aligned words past the last message
-  HIP_OK(hipMemcpyAsync(d.stage.p, base, total, hipMemcpyHostToDevice, w.stream));
+  // keys in the persistent key cache (pv_keycache_add): those signatures run
+  // the keyed latency kernel over a list, the others k_verify_quad_list; the
+  // image gets a tail of the uncached count, kidx[m] and the two lists (cached
+  // indices from the front, uncached from the back)
+  const size_t o_ext = (o_blob + bytes + 16 + 7) & ~size_t(7);
+  uint64_t nk = 0, ng = 0;
+  if (g_kc.count() && d.kc_count == g_kc.count() && d.lat_keyed_max && d.lat_quad) {
+    uint32_t* kidx = reinterpret_cast<uint32_t*>(base + o_ext + 8);
+    uint32_t* kl = kidx + m;
+    for (uint64_t i = 0; i < m; ++i) {
+      const uint32_t sl = g_kc.find(hb.pk + 32 * (s + i));
+      kidx[i] = sl == UINT32_MAX ? 0u : sl;
+      if (sl != UINT32_MAX) kl[nk++] = (uint32_t)i;
+      else kl[m - 1 - ng++] = (uint32_t)i;
+    }
+    *reinterpret_cast<uint64_t*>(base + o_ext) = ng;
+  }
   const uint8_t* g = d.stage.p;
-  const int rc = enqueue_verify(d, w, g + o_pk, g + o_sig, g + o_blob, reinterpret_cast<const uint64_t*>(g), m,
-                                d.verdict.p, nullptr, w.stream, false, nullptr, nullptr);
-  if (rc) return rc;
+  if (nk) {
+    const size_t total_ext = o_ext + 8 + 8 * m;
+    HIP_OK(hipMemcpyAsync(d.stage.p, base, total_ext, hipMemcpyHostToDevice, w.stream));
+    int rc = ws_begin(w, w.stream);
+    if (rc) return rc;
+    const uint64_t* goff = reinterpret_cast<const uint64_t*>(g);
+    const uint32_t* kidx = reinterpret_cast<const uint32_t*>(g + o_ext + 8);
+    HIP_OK(pv::launch_verify_quad_keyed(g + o_pk, false, g + o_sig, g + o_blob, goff, nk, kidx + m, d.kc.p, kidx,
+                                        d.bw.p, d.verdict.p, nullptr, w.stream));
+    if (ng)
+      HIP_OK(pv::launch_verify_quad_list(g + o_pk, g + o_sig, g + o_blob, goff, kidx + 2 * m - ng,
+                                         reinterpret_cast<const unsigned long long*>(g + o_ext), ng, (int)((ng + 7) / 8),
+                                         d.bw.p, d.verdict.p, d.mode == CurveMode::Full, w.stream));
+    rc = ws_end(w, w.stream);
+    if (rc) return rc;
+  } else {
+    HIP_OK(hipMemcpyAsync(d.stage.p, base, total, hipMemcpyHostToDevice, w.stream));
+    const int rc = enqueue_verify(d, w, g + o_pk, g + o_sig, g + o_blob, reinterpret_cast<const uint64_t*>(g), m,
+                                  d.verdict.p, nullptr, w.stream, false, nullptr, nullptr);
+    if (rc) return rc;
+  }
   HIP_OK(hipMemcpyAsync(d.vout.p, d.verdict.p, m, hipMemcpyDeviceToHost, w.stream));
   HIP_OK(hipStreamSynchronize(w.stream));
   memcpy(hb.verdict + s, d.vout.p, m);
@@ -1035,6 +1149,40 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   return PV_OK;
 }
 
+// prepare keys[0 .. count) (32 bytes each) into key-cache slots [first,
+// first + count) of device d, growing its table (existing slots are kept);
+// synchronous.  d.kc_count is left to the caller.
+int kc_prepare(Device& d, const uint8_t* keys, uint64_t first, uint64_t count) {
+  if (count == 0) return PV_OK;
+  HIP_OK(hipSetDevice(d.ord));
+  const uint64_t need = (first + count) * (uint64_t)pv::KEYTAB_WORDS;
+  if (need > d.kc.cap) {
+    size_t cap = d.kc.cap ? d.kc.cap : 64 * (size_t)pv::KEYTAB_WORDS;
+    while (cap < need) cap *= 2;
+    DevBuf<uint32_t> nb;
+    HIP_OK(nb.ensure(cap));
+    if (first) {
+      const hipError_t e = hipMemcpy(nb.p, d.kc.p, first * pv::KEYTAB_WORDS * sizeof(uint32_t), hipMemcpyDeviceToDevice);
+      if (e != hipSuccess) {
+        nb.release();
+        HIP_OK(e);
+      }
+    }
+    d.kc.release();
+    d.kc = nb;
+  }
+  int rc = ws_begin(d.ws[0], d.stream);
+  if (rc) return rc;
+  HIP_OK(d.kcpk.ensure(32 * count));
+  HIP_OK(hipMemcpyAsync(d.kcpk.p, keys, 32 * count, hipMemcpyHostToDevice, d.stream));
+  HIP_OK(d.kscr.ensure((count + 63) / 64 * 64 * pv::KEYTAB_SCRATCH));
+  HIP_OK(pv::launch_keys(d.kcpk.p, count, d.kc.p + first * pv::KEYTAB_WORDS, d.kscr.p, d.stream));
+  rc = ws_end(d.ws[0], d.stream);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(d.stream));
+  return PV_OK;
+}
+
 std::vector<Device*> select_devs(uint32_t mask) {
   std::vector<Device*> v;
   for (auto& d : g_devs)
@@ -1069,6 +1217,10 @@ int pv_init(uint32_t device_mask) {
     g_devs.back().id = id;
     g_devs.back().ord = dup ? 0 : id;
     int rc = init_device(g_devs.back());
+    if (rc == PV_OK && g_kc.count()) {   // a device added after keys were cached gets them too
+      rc = kc_prepare(g_devs.back(), g_kc.keys.data(), 0, g_kc.count());
+      if (rc == PV_OK) g_devs.back().kc_count = g_kc.count();
+    }
     if (rc != PV_OK) {
       release_device(g_devs.back());
       g_devs.pop_back();
@@ -1084,6 +1236,57 @@ void pv_shutdown(void) {
   DeviceGuard dg;
   for (auto& d : g_devs) release_device(d);
   g_devs.clear();
+  g_kc.clear();
+}
+
+int pv_keycache_add(const uint8_t* pk, uint64_t k) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (k == 0) return PV_OK;
+  if (!pk) return fail(PV_EINVAL, "null buffer");
+  if (g_kc.count() + k > 0xfffffffeull) return fail(PV_EINVAL, "key cache limited to 2^32 - 2 keys");
+  // keys not cached yet, first occurrence only
+  std::vector<uint8_t> add;
+  {
+    KeyIndex seen;
+    seen.reset(pk, k);
+    for (uint64_t i = 0; i < k; ++i) {
+      const size_t before = seen.first.size();
+      (void)seen.insert(i);
+      if (seen.first.size() != before && g_kc.find(pk + 32 * i) == UINT32_MAX)
+        add.insert(add.end(), pk + 32 * i, pk + 32 * i + 32);
+    }
+  }
+  if (add.empty()) return PV_OK;
+  const uint64_t first = g_kc.count(), cnt = add.size() / 32;
+  for (auto& d : g_devs) {
+    const int rc = kc_prepare(d, add.data(), first, cnt);
+    if (rc) return rc;   // committed nowhere: every device keeps its previous slots
+  }
+  g_kc.commit(add);
+  for (auto& d : g_devs) d.kc_count = g_kc.count();
+  return PV_OK;
+}
+
+int pv_keycache_clear(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  g_kc.clear();
+  for (auto& d : g_devs) {
+    (void)hipSetDevice(d.ord);
+    (void)hipStreamSynchronize(d.stream);
+    d.kc.release();
+    d.kc_count = 0;
+  }
+  return PV_OK;
+}
+
+int pv_keycache_size(uint64_t* count) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!count) return fail(PV_EINVAL, "null buffer");
+  *count = g_kc.count();
+  return PV_OK;
 }
 
 const char* pv_last_error(void) { return g_err.c_str(); }
@@ -1343,6 +1546,14 @@ int pv_set_lat_max(uint64_t max_signatures) {
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
   if (max_signatures > (1ull << 20)) return fail(PV_EINVAL, "max_signatures must be <= 2^20");
   for (auto& d : g_devs) d.lat_max = max_signatures;
+  return PV_OK;
+}
+
+int pv_set_lat_keyed_max(uint64_t max_signatures) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
+  if (max_signatures > (1ull << 20)) return fail(PV_EINVAL, "max_signatures must be <= 2^20");
+  for (auto& d : g_devs) d.lat_keyed_max = max_signatures;
   return PV_OK;
 }
 

@@ -105,6 +105,15 @@ hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32
 constexpr int KEYTAB_WORDS = 8 * 9 * 32 + 32;
 constexpr int KEYTAB_SCRATCH = 64 * 40;   // projective entries + prefix products (lane-interleaved per 64 keys)
 hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
+// latency mode for prepared keys (k_verify_quad_keyed): the whole verify of n
+// signatures in one launch, signature e's key = ktab entry kidx[i] with i =
+// list ? list[e] : e; the hashed key bytes are pk + 32 * (pk_by_key ? kidx[i] : i).
+// Verdicts go to verdict[i]; bitmap (ceil(n/64) words, needs no zeroing) only
+// without a list (may be NULL then too)
+hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uint8_t* sig, const uint8_t* blob,
+                                    const uint64_t* off, uint64_t n, const uint32_t* list, const uint32_t* ktab,
+                                    const uint32_t* kidx, const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap,
+                                    hipStream_t s);
 
 // keygen + sign: pk[i], sig[i] for seed[i] over M_i
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n,

@@ -847,6 +847,100 @@ hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* 
   return hipGetLastError();
 }
 
+// k_verify_quad_keyed: the latency verdict of signatures whose key is
+// prepared (pv_quad.h q_keyed_side).  A block of 128 threads takes 8
+// signatures: wave 1 (one lane per signature) runs the pre-checks, SHA-512
+// and h mod L into an LDS record while wave 0 (8 lanes per signature) decodes
+// -R; after one barrier each quad runs its half of the comb (28 doublings, 40
+// affine adds), side 1 adds -R and side 0 tests the sum for the identity.
+// LIST: signature e of the launch is list[e] (host-buffer calls whose batch
+// mixes cached and uncached keys); else e itself, and the verdict bits also
+// go to the bitmap as the block's byte.
+template <bool LIST>
+__global__ __launch_bounds__(128) void k_verify_quad_keyed(const uint8_t* __restrict__ pk, int pk_by_key,
+                                                           const uint8_t* __restrict__ sig,
+                                                           const uint8_t* __restrict__ blob,
+                                                           const uint64_t* __restrict__ off, uint64_t n,
+                                                           const uint32_t* __restrict__ list,
+                                                           const uint32_t* __restrict__ ktab,
+                                                           const uint32_t* __restrict__ kidx,
+                                                           const uint32_t* __restrict__ bw, uint8_t* __restrict__ verdict,
+                                                           uint8_t* __restrict__ bitmap_bytes, uint64_t bitmap_len) {
+  __shared__ uint32_t recs[8 * KQ_WORDS];
+  const int t = (int)threadIdx.x;
+  const uint64_t e0 = (uint64_t)blockIdx.x * 8;
+  const int side = (t >> 2) & 1;
+  const QRole q = qrole_of((uint32_t)t & 3u);
+  const uint64_t e = e0 + (uint64_t)((t & 63) >> 3);
+  const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
+  const uint64_t ic = LIST ? list[ec] : ec;
+  qfe R, eR;
+  bool okR = false;
+  if (t >= 64) {
+    // wave 1: the scalar stage, lane k for signature e0 + k
+    const int k = t - 64;
+    if (k < 8) {
+      uint32_t* r = recs + KQ_WORDS * k;
+      const uint64_t ek = e0 + (uint64_t)k;
+      uint32_t dig[16];
+      bool pre = false;
+      uint64_t j = 0;
+      if (ek < n) {
+        j = LIST ? list[ek] : ek;
+        const uint8_t* a = pk + 32 * (pk_by_key ? (uint64_t)kidx[j] : j);
+        pre = hash_one(dig, a, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
+      }
+      keyed_record(r, pre, dig, sig + 64 * j);
+    }
+  } else {
+    // wave 0: -R (both quads of a signature decode it; side 1 adds it)
+    okR = q_decode_neg(R, sig + 64 * ic, true, q);
+    q_to_cached(eR, R, q);
+  }
+  __syncthreads();
+  if (t >= 64) return;
+  const uint32_t* r = recs + KQ_WORDS * (t >> 3);
+  const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
+  qfe acc, x, x1;
+  q_keyed_side(acc, eR, r, side, kt, bw, q);
+  q_to_cached(x, acc, q);
+#pragma unroll
+  for (int k = 0; k < 10; ++k) x1.l[0].v[k] = __shfl_xor(x.l[0].v[k], 4, 64);   // side 1 -> side 0
+  const bool id = q_sum_is_identity(acc, x1, q);
+  const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && okR && id;
+  const bool mine = side == 0 && (t & 3) == 0 && e < n;
+  if (mine) verdict[ic] = v ? 1 : 0;
+  if constexpr (!LIST) {
+    const uint64_t ball = __ballot(mine && v);   // bits 8k: signature e0 + k
+    if (t == 0 && bitmap_bytes) {
+      uint32_t bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bits |= (uint32_t)((ball >> (8 * k)) & 1ull) << k;
+      bitmap_bytes[blockIdx.x] = (uint8_t)bits;
+      if ((uint64_t)blockIdx.x + 1 == gridDim.x)
+        for (uint64_t b = (uint64_t)blockIdx.x + 1; b < bitmap_len; ++b) bitmap_bytes[b] = 0;
+    }
+  }
+}
+
+hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uint8_t* sig, const uint8_t* blob,
+                                    const uint64_t* off, uint64_t n, const uint32_t* list, const uint32_t* ktab,
+                                    const uint32_t* kidx, const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap,
+                                    hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + 7) / 8;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  if (list && bitmap) return hipErrorInvalidValue;
+  const uint64_t bytes = (n + 63) / 64 * 8;
+  if (list)
+    hipLaunchKernelGGL(k_verify_quad_keyed<true>, dim3((uint32_t)blocks), dim3(128), 0, s, pk, pk_by_key ? 1 : 0, sig,
+                       blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0);
+  else
+    hipLaunchKernelGGL(k_verify_quad_keyed<false>, dim3((uint32_t)blocks), dim3(128), 0, s, pk, pk_by_key ? 1 : 0,
+                       sig, blob, off, n, nullptr, ktab, kidx, bw, verdict, reinterpret_cast<uint8_t*>(bitmap), bytes);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------- batch signer
 __global__ __launch_bounds__(256) void k_sign(const uint8_t* __restrict__ seeds, const uint8_t* __restrict__ blob,
                                                const uint64_t* __restrict__ off, uint64_t n,

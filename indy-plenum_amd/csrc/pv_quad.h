@@ -277,18 +277,25 @@ PV_HD int q_digit(const uint32_t dw[8], int w) { return (int)((pick8(dw, w >> 3)
 // decode side's point (-A, or -R with canonical y) and write its cached
 // multiples 0..8 to the quad table `tab` (QTAB_WORDS, each lane its
 // coordinate); Q = the point.  false = does not decode.
-PV_HD bool q_side_table(qfe& Q, const uint8_t* pk, const uint8_t* sig, int side, uint32_t* tab, const QRole& q) {
+// Q = -P for the 32-byte encoding at `enc` (every lane of the quad decodes the
+// point: the chain is serial anyway); canon: also require y < p (R's rule).
+// false = does not decode.
+PV_HD bool q_decode_neg(qfe& Q, const uint8_t* enc_bytes, bool canon, const QRole& q) {
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < QL; ++j) {
-    // every lane of the quad decodes the point (the chain is serial anyway)
     uint32_t enc[8];
-    load8(enc, side ? sig : pk);
+    load8(enc, enc_bytes);
     ge_p3 P;
     const bool dec = ge_frombytes_negate(P, enc);
-    ok = dec && (side == 0 || y_is_canonical(enc));
+    ok = dec && (!canon || y_is_canonical(enc));
     role_coord(Q.l[j], P, qrole(j, q));
   }
+  return ok;
+}
+
+PV_HD bool q_side_table(qfe& Q, const uint8_t* pk, const uint8_t* sig, int side, uint32_t* tab, const QRole& q) {
+  const bool ok = q_decode_neg(Q, side ? sig : pk, side != 0, q);
   qfe e1, e, acc;
   q_to_cached(e1, Q, q);
 #pragma unroll
@@ -395,6 +402,105 @@ PV_HD bool q_sum_is_identity(const qfe& Q0, const qfe& e1, const QRole& q) {
     id = p1p1_is_identity(t);
   }
   return id;
+}
+
+// ------------------------------------------------------- prepared keys
+// Latency verdict of a signature whose key is in the device key cache
+// (k_verify_quad_keyed): -A is never decompressed.  The key's 8-way comb
+// tables (key_prepare: k 2^(32 q) (-A), affine niels) and the radix-2^16
+// chunk tables of B give R' = h(-A) + S B in 28 doublings and 80 affine adds
+// (double_scalarmult_comb's schedule), split over the signature's two quads:
+// side s adds the key tables and the base-point chunks q = 4s .. 4s + 3, so a
+// lane runs 28 (sq + mul) + 40 x 2 mul.  libsodium accepts iff encode(R') ==
+// R, i.e. iff R decodes with a canonical y and R' + (-R) = O (the identity
+// test of the half-size path, pv_lattice.h): -R is decoded while the scalar
+// wave hashes, side 1 adds it, and side 0 tests Q0 + Q1 = O.
+//
+// record (LDS): h + the radix-16 digit offsets (8 words), S + the radix-2^16
+// digit offsets (8 words), pre-check verdict
+constexpr int KQ_H = 0, KQ_S = 8, KQ_OK = 16, KQ_WORDS = 17;
+
+PV_HD void keyed_record(uint32_t* rec, bool pre, const uint32_t dig[16], const uint8_t* sig) {
+  uint32_t hh[8], S[8];
+  if (pre) {
+    sc_reduce64(hh, dig);            // h = SHA-512(R||A||M) mod L (App. C.2 step 5)
+    load8(S, sig + 32);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hh[k] = S[k] = 0;
+  }
+  sc_add_pattern(hh, hh, 0x88888888u);
+  sc_add_pattern(S, S, HALF_S_PATTERN);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    rec[KQ_H + k] = hh[k];
+    rec[KQ_S + k] = S[k];
+  }
+  rec[KQ_OK] = pre ? 1u : 0u;
+}
+
+// side's share of the comb: kt = the key's comb tables, bw = the chunk tables
+// of B.  Each window's entries (4 key, and on windows 4 and 0 four base-point
+// entries) are fetched before its four doublings.
+PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* kt, const uint32_t* bw,
+                       const QRole& q) {
+  uint32_t hp[4], sp[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hp[k] = rec[KQ_H + 4 * side + k];
+    sp[k] = rec[KQ_S + 4 * side + k];
+  }
+  const uint32_t* kts = kt + 4 * side * KT_TABLE;
+  const uint32_t* bws = bw + (uint64_t)(4 * side) * BW_TABLE;
+#pragma unroll
+  for (int j = 0; j < QL; ++j) role_p3_identity(acc.l[j], qrole(j, q));
+#pragma unroll 1
+  for (int w = 7; w >= 0; --w) {
+    qfe ek[4], eb[4];
+    int dk[4], db[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      dk[k] = (int)((hp[k] >> (4 * w)) & 15u) - 8;
+      q_load_niels(ek[k], kts + k * KT_TABLE + (dk[k] < 0 ? -dk[k] : dk[k]) * KT_ENTRY, dk[k] < 0, q);
+    }
+    const bool bwin = (w & 3) == 0;
+    if (bwin) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        db[k] = (int)((sp[k] >> (4 * w)) & 0xffffu) - 32768;   // w = 4: high halves, w = 0: low
+        q_load_niels(eb[k], bws + (uint64_t)k * BW_TABLE + (uint64_t)(db[k] < 0 ? -db[k] : db[k]) * BT_WORDS,
+                     db[k] < 0, q);
+      }
+    }
+    if (w != 7) {
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) q_dbl(acc, q);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q_add(acc, ek[k], dk[k] < 0, q);
+    if (bwin) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q_add(acc, eb[k], db[k] < 0, q);
+    }
+  }
+}
+
+// side's point of the keyed verdict: its comb share, plus -R on side 1
+// (eR = -R in cached add order; side 0 adds the identity: the same
+// instruction stream on both quads)
+PV_HD void q_keyed_side(qfe& acc, const qfe& eR, const uint32_t* rec, int side, const uint32_t* kt,
+                        const uint32_t* bw, const QRole& q) {
+  q_comb_side(acc, rec, side, kt, bw, q);
+  const uint32_t sm = 0u - (uint32_t)(side != 0);
+  qfe e;
+#pragma unroll
+  for (int j = 0; j < QL; ++j) {
+    fe id;
+    role_cached_identity(id, qrole(j, q));
+#pragma unroll
+    for (int i = 0; i < 10; ++i) e.l[j].v[i] = bitsel(sm, eR.l[j].v[i], id.v[i]);
+  }
+  q_add(acc, e, false, q);
 }
 
 }  // namespace pv

@@ -66,6 +66,10 @@ SIGNATURES = [
     ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_set_lat_max', ctypes.c_int, [ctypes.c_uint64]),
     ('pv_set_lat_kernel', ctypes.c_int, [ctypes.c_uint32]),
+    ('pv_set_lat_keyed_max', ctypes.c_int, [ctypes.c_uint64]),
+    ('pv_keycache_add', ctypes.c_int, [_vp, ctypes.c_uint64]),
+    ('pv_keycache_clear', ctypes.c_int, []),
+    ('pv_keycache_size', ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     ('pv_set_host_fused', ctypes.c_int, [ctypes.c_int]),
     ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
     ('pv_bls_set_keys', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
@@ -111,6 +115,62 @@ def set_lat_max(max_signatures):
     """Largest generic batch that runs the latency-mode curve kernel (8 lanes
     per signature) on every initialised device; 0 disables (pv_set_lat_max)."""
     _check('pv_set_lat_max', load().pv_set_lat_max(int(max_signatures)))
+
+
+LAT_KEYED_MAX_DEFAULT = 8192   # PV_LAT_KEYED_MAX in csrc/pv_api.cpp
+
+
+def set_lat_keyed_max(max_signatures):
+    """Largest keyed batch (prepared keys) that runs the keyed latency kernel
+    on every initialised device; 0 disables (pv_set_lat_keyed_max)."""
+    _check('pv_set_lat_keyed_max', load().pv_set_lat_keyed_max(int(max_signatures)))
+
+
+def keycache_add(keys):
+    """Add 32-byte verifying keys (an (k, 32) u8 array or an iterable of bytes)
+    to the persistent device key cache (pv_keycache_add); cached keys are skipped."""
+    ensure_init()
+    if not isinstance(keys, np.ndarray):
+        keys = [bytes(k) for k in keys]
+        if any(len(k) != 32 for k in keys):
+            raise ValueError('verifying keys are 32 bytes')
+        keys = np.frombuffer(b''.join(keys), np.uint8) if keys else np.zeros(0, np.uint8)
+    keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
+    if keys.shape[0]:
+        _check('pv_keycache_add', load().pv_keycache_add(_ptr(keys), keys.shape[0]))
+
+
+_pending_keys = []   # keys registered before / between GPU calls (keycache_defer)
+
+
+def keycache_defer(raw):
+    """Queue a 32-byte key for the device key cache; it is added by the next
+    host-buffer verify call (no GPU work here: addIdr may run before pv_init)."""
+    raw = bytes(raw)
+    if len(raw) == 32:
+        with _lock:
+            _pending_keys.append(raw)
+
+
+def _flush_keycache():
+    if _pending_keys:
+        with _lock:
+            keys = list(_pending_keys)
+            _pending_keys.clear()
+        keycache_add(keys)
+
+
+def keycache_clear():
+    with _lock:
+        _pending_keys.clear()
+    if _inited_mask is not None:
+        _check('pv_keycache_clear', load().pv_keycache_clear())
+
+
+def keycache_size():
+    c = ctypes.c_uint64()
+    _check('pv_keycache_size', load().pv_keycache_size(ctypes.byref(c)))
+    return c.value
 
 
 LAT_KERNELS = {'quad': 0, 'pair': 1}   # PV_LAT_QUAD / PV_LAT_PAIR
@@ -262,6 +322,7 @@ def verify_batch_arrays(pk, sig, blob, off, device_mask=0, dedup_keys=True):
     verdict = np.zeros(n, dtype=np.uint8)
     if n == 0:
         return verdict.astype(bool)
+    _flush_keycache()
     flags = PV_FLAG_DEDUP_KEYS if dedup_keys else 0
     _check('pv_verify_batch', load().pv_verify_batch(_ptr(pk), _ptr(sig), _ptr(blob), _ptr(off), n, _ptr(verdict),
                                                       device_mask, flags))

@@ -31,7 +31,7 @@ from .exceptions import (CouldNotAuthenticate, EmptyIdentifier, EmptySignature, 
 from . import nacl_wrappers
 from .nacl_wrappers import SIGN_BYTES
 from .serialization import serialize_msg_for_signing
-from .verifier import DidVerifier, Verifier
+from .verifier import DidVerifier, Verifier, resolve_verkey
 
 
 # ----------------------------------------------------------- state helpers
@@ -242,6 +242,15 @@ class SimpleAuthNr(NaclAuthNr):
 
     def addIdr(self, identifier, verkey, role=None):
         self.clients[identifier] = {VERKEY: verkey, ROLE: role}
+        # a registered DID's key goes to the device key cache (nacl_wrappers.
+        # cache_verkeys); a key that does not resolve is left to the request
+        # path, which raises exactly as the reference does
+        try:
+            raw = base58.b58decode(resolve_verkey(verkey, identifier))
+        except Exception:
+            return
+        if len(raw) == nacl_wrappers.PUBLICKEY_BYTES:
+            nacl_wrappers.cache_verkeys([raw])
 
     def getVerkey(self, ident, request):
         nym = self.clients.get(ident)

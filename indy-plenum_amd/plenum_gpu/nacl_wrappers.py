@@ -77,6 +77,18 @@ def verify_signed_batch(items):
     return out
 
 
+def cache_verkeys(keys):
+    """Put 32-byte verifying keys a node already knows (node keys, client DIDs,
+    NYM verkeys) in the persistent device key cache (pv_keycache_add): small
+    host calls under them skip the decompression of A.  Verdicts are unchanged.
+    No GPU work happens here; the keys are added by the next verify call."""
+    for k in keys:
+        k = bytes(k)
+        if len(k) != PUBLICKEY_BYTES:
+            raise ValueError('The key must be exactly %s bytes long' % PUBLICKEY_BYTES)
+        _native.keycache_defer(k)
+
+
 def crypto_sign_open(sm, pk):
     """libnacl.crypto_sign_open contract: the message, or ValueError."""
     if not verify_signed_batch([(bytes(pk), bytes(sm))])[0]:

@@ -1,0 +1,104 @@
+"""Keyed latency kernel (k_verify_quad_keyed) and the persistent device key
+cache of host-buffer calls (pv_keycache_add): verdicts must equal the
+libsodium-1.0.18 fixtures whatever mix of cached / uncached keys a call holds,
+and the device keyed path of small batches must equal the synthetic spec and
+the keyed throughput kernel (PV_LAT_KEYED_MAX = 0)."""
+import numpy as np
+import pytest
+
+from conftest import split_sm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def nat():
+    from plenum_gpu import _native as nat
+    nat.ensure_init()
+    nat.keycache_clear()
+    yield nat
+    nat.keycache_clear()
+    nat.set_lat_keyed_max(nat.LAT_KEYED_MAX_DEFAULT)
+
+
+def _slice(r, start, n):
+    o = r['off'][start:start + n + 1]
+    return r['pk'][start:start + n], r['sig'][start:start + n], r['blob'][int(o[0]):int(o[-1])], o - o[0]
+
+
+def test_cached_keys_raw_vectors(nat, raw_vectors):
+    """Every raw-vector key cached: ragged Looper-pass sizes through the keyed
+    latency kernel, then half the keys cached (each call mixes the keyed and
+    the generic list kernel), then none; always the fixture's verdicts."""
+    r = raw_vectors
+    want = r['verdict'].astype(bool)
+    sizes = ((0, 1), (5, 7), (11, 8), (100, 9), (200, 100), (1000, 1000), (17, 2048), (0, 3000))
+    nat.keycache_add(r['pk'])
+    assert nat.keycache_size() == len(np.unique(r['pk'], axis=0))
+    for start, n in sizes:
+        got = nat.verify_batch_arrays(*_slice(r, start, n))
+        assert (got == want[start:start + n]).all(), ('all cached', start, n)
+    nat.keycache_clear()
+    nat.keycache_add(r['pk'][::2])
+    for start, n in sizes:
+        got = nat.verify_batch_arrays(*_slice(r, start, n))
+        assert (got == want[start:start + n]).all(), ('half cached', start, n)
+    nat.keycache_clear()
+    assert nat.keycache_size() == 0
+    got = nat.verify_batch_arrays(*_slice(r, 0, 3000))
+    assert (got == want).all()
+
+
+def test_cached_keys_adversarial(nat, adversarial):
+    """The adversarial fixture with every key cached: keys libsodium refuses
+    (small order, non-canonical, not on the curve, the blocklist) are cached as
+    refused, mixed-order keys keep their cofactorless verdicts, R edge cases
+    (non-canonical y, small order, off curve) take the decode of -R."""
+    from plenum_gpu.nacl_wrappers import verify_signed_batch
+    rows = split_sm(adversarial)
+    nat.keycache_add([pk for _, pk, _, _ in rows])
+    got = verify_signed_batch([(pk, sm) for _, pk, sm, _ in rows])
+    wrong = [rows[k][0] for k in range(len(rows)) if got[k] != rows[k][3]]
+    assert not wrong, wrong
+    # one signature at a time (the per-request Node.verifySignature shape)
+    for k in range(0, len(rows), 7):
+        _, pk, sm, v = rows[k]
+        assert bool(verify_signed_batch([(pk, sm)])[0]) == v, rows[k][0]
+
+
+def test_keycache_dedup_and_add_idr(nat, raw_vectors):
+    """Adding cached keys again changes nothing; SimpleAuthNr.addIdr queues the
+    registered DID's key and the next verify call adds it."""
+    from plenum_gpu import base58
+    from plenum_gpu.client_authn import SimpleAuthNr
+    r = raw_vectors
+    nat.keycache_add(r['pk'][:10])
+    nat.keycache_add(np.concatenate([r['pk'][:10], r['pk'][:10]]))
+    assert nat.keycache_size() == len(np.unique(r['pk'][:10], axis=0))
+    a = SimpleAuthNr()
+    a.addIdr('did1', base58.b58encode(bytes(r['pk'][20])).decode())
+    a.addIdr('did2', 'not base58 0OIl')   # resolves to nothing: left to the request path
+    got = nat.verify_batch_arrays(*_slice(r, 20, 1))
+    assert got[0] == bool(r['verdict'][20])
+    assert nat.keycache_size() == len(np.unique(r['pk'][:10], axis=0)) + 1
+
+
+@pytest.mark.parametrize('n', [1, 8, 100, 1000, 8192])
+def test_keyed_device_latency_kernel(nat, n):
+    """Device keyed batches up to PV_LAT_KEYED_MAX take k_verify_quad_keyed:
+    verdicts and bitmap equal the synthetic spec (~5 % tampered) and the keyed
+    throughput kernel (latency path disabled)."""
+    from plenum_gpu.device import SyntheticBatch
+    b = SyntheticBatch(0, n, 256, cfg=6, first=4242, key_mod=max(1, n // 8))
+    assert b.use_key_cache(True)
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    res = []
+    for lat in (nat.LAT_KEYED_MAX_DEFAULT, 0):
+        nat.set_lat_keyed_max(lat)
+        b.bitmap.fill_(-1)
+        v = b.verify().cpu().numpy().astype(bool)
+        bits = np.unpackbits(b.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:n].astype(bool)
+        assert (v == want).all(), lat
+        assert (bits == v).all(), lat
+        res.append(v)
+    assert (res[0] == res[1]).all()

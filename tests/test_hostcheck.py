@@ -370,6 +370,41 @@ def test_keyed_path_adversarial_bit_exact(hc, adversarial):
     assert (v.astype(bool) == want).all()
 
 
+def _run_keyed_quad(hc, pk, sig, blob, off):
+    upk, kidx = np.unique(pk, axis=0, return_inverse=True)
+    kidx = np.ascontiguousarray(kidx.reshape(-1), np.uint32)
+    upk = np.ascontiguousarray(upk, np.uint8)
+    n = len(pk)
+    v = np.zeros(n, np.uint8)
+    b = orc.padded(blob)
+    hc.hc_reset_counts()
+    hc.hc_verify_keyed_quad(_p(upk), ctypes.c_uint64(len(upk)), _p(kidx), _p(np.ascontiguousarray(sig)), _p(b),
+                            _p(np.ascontiguousarray(off)), ctypes.c_uint64(n), _p(v))
+    _, bad = counts(hc)
+    assert bad == 0
+    return v
+
+
+def test_keyed_quad_schedule_adversarial_bit_exact(hc, adversarial):
+    """Keyed latency kernel's schedule (k_verify_quad_keyed, pv_quad.h
+    q_keyed_side: each side's comb share on an emulated lane quad, -R added on
+    side 1, identity test): every adversarial case gives the fixture's verdict,
+    every multiply bound-checked."""
+    pk, sig, blob, off, want = _adv_arrays(adversarial)
+    v = _run_keyed_quad(hc, pk, sig, blob, off)
+    assert (v.astype(bool) == want).all()
+
+
+def test_keyed_quad_schedule_raw_vectors(hc, raw_vectors):
+    r = raw_vectors
+    sel = slice(0, 600)
+    pk, sig = r['pk'][sel], r['sig'][sel]
+    off = r['off'][:601] - r['off'][0]
+    blob = r['blob'][int(r['off'][0]):int(r['off'][600])]
+    v = _run_keyed_quad(hc, pk, sig, blob, off)
+    assert (v == r['verdict'][sel]).all()
+
+
 def test_op_counts_pin_keyed_constants(hc):
     """Work split of the prepared-key (comb) path (bench.py W_*_KEYED / W_*_KEYPREP):
     16 signatures under ONE prepared key vs 16 keys prepared."""

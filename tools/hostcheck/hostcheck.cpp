@@ -253,6 +253,32 @@ void hc_verify_keyed(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const 
   free(pre);
 }
 
+// keyed latency kernel (k_verify_quad_keyed): prepared keys, each side's
+// comb share on an emulated quad, -R added on side 1, identity test
+void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
+                          const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* verdict) {
+  ensure_btab();
+  uint32_t* ktab = (uint32_t*)calloc(k ? k * KEY_WORDS : KEY_WORDS, sizeof(uint32_t));
+  uint32_t* scr = (uint32_t*)calloc(KEY_SCRATCH, sizeof(uint32_t));
+  for (uint64_t j = 0; j < k; ++j) key_prepare(ktab + j * KEY_WORDS, scr, pk + 32 * j);
+  free(scr);
+  const QRole qr = qrole_of(0);
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t dig[16], rec[KQ_WORDS];
+    const bool pre = hash_one(dig, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+    keyed_record(rec, pre, dig, sig + 64 * i);
+    qfe R, eR, Q0, Q1, x1;
+    const bool okR = q_decode_neg(R, sig + 64 * i, true, qr);
+    q_to_cached(eR, R, qr);
+    const uint32_t* kt = ktab + (uint64_t)kidx[i] * KEY_WORDS;
+    q_keyed_side(Q0, eR, rec, 0, kt, g_bw, qr);
+    q_keyed_side(Q1, eR, rec, 1, kt, g_bw, qr);
+    q_to_cached(x1, Q1, qr);
+    verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && okR && q_sum_is_identity(Q0, x1, qr)) ? 1 : 0;
+  }
+  free(ktab);
+}
+
 // SHA-256(prefix || M_i) with the kernels' block loader; prefix < 0 = none
 void hc_sha256(const uint8_t* blob, const uint64_t* off, uint64_t n, int prefix, uint8_t* out) {
   for (uint64_t i = 0; i < n; ++i)
