@@ -57,6 +57,11 @@ int fail(int code, const char* fmt, ...) {
 // keyed batches (prepared keys) of at most this many signatures run the keyed
 // latency kernel (k_verify_quad_keyed); PV_LAT_KEYED_MAX env overrides (0 disables)
 #define PV_LAT_KEYED_MAX 8192
+// host-buffer calls of at most this many signatures skip the H2D / D2H copies:
+// the latency kernel reads the gathered inputs from, and writes the verdicts
+// to, fine-grained page-locked host memory (one launch per call instead of
+// copy + launch + copy); PV_SMALL_ZC_MAX env overrides (0 = always copy)
+#define PV_SMALL_ZC_MAX 2048
 // shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
 #define PV_DEDUP_SAMPLE_MIN 262144
 // chunk gathers into the pinned staging ring use up to this many host threads
@@ -101,12 +106,13 @@ struct DevBuf {
 struct PinBuf {
   uint8_t* p = nullptr;
   size_t cap = 0;  // bytes
+  unsigned flags = hipHostMallocDefault;
   hipError_t ensure(size_t n) {
     if (n <= cap && p) return hipSuccess;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), n, flags);
     if (e == hipSuccess) cap = n;
     return e;
   }
@@ -401,6 +407,8 @@ struct Device {
   size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
   uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; PV_LAT_MAX env (0 = off)
   uint64_t lat_keyed_max = PV_LAT_KEYED_MAX;  // keyed batches up to this size: k_verify_quad_keyed
+  uint64_t zc_max = PV_SMALL_ZC_MAX;          // host calls up to this size: zero-copy (PV_SMALL_ZC_MAX env)
+  PinBuf zc_in, zc_out;                       // fine-grained page-locked image / verdicts of zero-copy calls
   bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
   // host-buffer chunks of generic batches: one k_chunk_half launch per chunk
   // + one k_verify_quad_list pass for the deferred records; PV_HOST_FUSED=0:
@@ -513,6 +521,12 @@ int init_device(Device& d) {
     if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_KEYED_MAX must be in 0..1048576 (got %s)", t);
     d.lat_keyed_max = (uint64_t)v;
   }
+  if (const char* t = getenv("PV_SMALL_ZC_MAX")) {
+    const long v = atol(t);
+    if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_SMALL_ZC_MAX must be in 0..1048576 (got %s)", t);
+    d.zc_max = (uint64_t)v;
+  }
+  d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped;
   if (const char* t = getenv("PV_HOST_FUSED")) {
     if (strcmp(t, "0") != 0 && strcmp(t, "1") != 0) return fail(PV_EINVAL, "PV_HOST_FUSED must be 0 or 1 (got %s)", t);
     d.chunk_fused = t[0] == '1';
@@ -614,6 +628,8 @@ void release_device(Device& d) {
   d.dl.release(); d.dlc.release();
   d.pin[0].release();
   d.pin[1].release();
+  d.zc_in.release();
+  d.zc_out.release();
   d.vout.release();
   if (d.pool) d.pool->shutdown();
   d.copy = nullptr;
@@ -837,13 +853,32 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   } drain{d};
   const uint64_t b0 = hb.off[s], bytes = hb.off[e] - b0;
   const size_t o_pk = (m + 1) * 8, o_sig = o_pk + m * 32, o_blob = o_sig + m * 64, total = small_bytes(hb, s, e);
-  if (d.pin[0].ensure(total) != hipSuccess || d.vout.ensure(m) != hipSuccess) {
+  // zero-copy: the kernels read the image from and write the verdicts to
+  // fine-grained host memory (no copy launches); else one H2D into `stage`
+  // and one D2H of the verdicts
+  const bool zc = m <= d.zc_max;
+  PinBuf& pin = zc ? d.zc_in : d.pin[0];
+  PinBuf& vout = zc ? d.zc_out : d.vout;
+  if (pin.ensure(total) != hipSuccess || vout.ensure(m) != hipSuccess) {
     (void)hipGetLastError();
     return 1;
   }
-  HIP_OK(d.stage.ensure(total));
-  HIP_OK(d.verdict.ensure(m));
-  uint8_t* base = d.pin[0].p;
+  uint8_t* base = pin.p;
+  const uint8_t* g = nullptr;
+  uint8_t* vdst = nullptr;
+  if (zc) {
+    void* a = nullptr;
+    void* b = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&a, pin.p, 0));
+    HIP_OK(hipHostGetDevicePointer(&b, vout.p, 0));
+    g = static_cast<const uint8_t*>(a);
+    vdst = static_cast<uint8_t*>(b);
+  } else {
+    HIP_OK(d.stage.ensure(total));
+    HIP_OK(d.verdict.ensure(m));
+    g = d.stage.p;
+    vdst = d.verdict.p;
+  }
   std::atomic<bool> bad{false};
   const CopyJob jobs[4] = {{base, reinterpret_cast<const uint8_t*>(hb.off + s), (m + 1) * 8, b0, true},
                            {base + o_pk, hb.pk + 32 * s, m * 32},
@@ -870,31 +905,30 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     }
     *reinterpret_cast<uint64_t*>(base + o_ext) = ng;
   }
-  const uint8_t* g = d.stage.p;
   if (nk) {
     const size_t total_ext = o_ext + 8 + 8 * m;
-    HIP_OK(hipMemcpyAsync(d.stage.p, base, total_ext, hipMemcpyHostToDevice, w.stream));
+    if (!zc) HIP_OK(hipMemcpyAsync(d.stage.p, base, total_ext, hipMemcpyHostToDevice, w.stream));
     int rc = ws_begin(w, w.stream);
     if (rc) return rc;
     const uint64_t* goff = reinterpret_cast<const uint64_t*>(g);
     const uint32_t* kidx = reinterpret_cast<const uint32_t*>(g + o_ext + 8);
     HIP_OK(pv::launch_verify_quad_keyed(g + o_pk, false, g + o_sig, g + o_blob, goff, nk, kidx + m, d.kc.p, kidx,
-                                        d.bw.p, d.verdict.p, nullptr, w.stream));
+                                        d.bw.p, vdst, nullptr, w.stream));
     if (ng)
       HIP_OK(pv::launch_verify_quad_list(g + o_pk, g + o_sig, g + o_blob, goff, kidx + 2 * m - ng,
                                          reinterpret_cast<const unsigned long long*>(g + o_ext), ng, (int)((ng + 7) / 8),
-                                         d.bw.p, d.verdict.p, d.mode == CurveMode::Full, w.stream));
+                                         d.bw.p, vdst, d.mode == CurveMode::Full, w.stream));
     rc = ws_end(w, w.stream);
     if (rc) return rc;
   } else {
-    HIP_OK(hipMemcpyAsync(d.stage.p, base, total, hipMemcpyHostToDevice, w.stream));
+    if (!zc) HIP_OK(hipMemcpyAsync(d.stage.p, base, total, hipMemcpyHostToDevice, w.stream));
     const int rc = enqueue_verify(d, w, g + o_pk, g + o_sig, g + o_blob, reinterpret_cast<const uint64_t*>(g), m,
-                                  d.verdict.p, nullptr, w.stream, false, nullptr, nullptr);
+                                  vdst, nullptr, w.stream, false, nullptr, nullptr);
     if (rc) return rc;
   }
-  HIP_OK(hipMemcpyAsync(d.vout.p, d.verdict.p, m, hipMemcpyDeviceToHost, w.stream));
+  if (!zc) HIP_OK(hipMemcpyAsync(vout.p, d.verdict.p, m, hipMemcpyDeviceToHost, w.stream));
   HIP_OK(hipStreamSynchronize(w.stream));
-  memcpy(hb.verdict + s, d.vout.p, m);
+  memcpy(hb.verdict + s, vout.p, m);
   return PV_OK;
 }
 

@@ -145,31 +145,61 @@ PV_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q, bool neg) {
 // Restates ge25519_frombytes_negate_vartime's contract (SURVEY.md App. C.2
 // step 4): fails iff (y^2-1)/(dy^2+1) has no square root; x == 0 with the
 // sign bit set is accepted (libsodium 1.0.18).
-PV_HD bool ge_frombytes_negate(ge_p3& h, const uint32_t s[8]) {
-  fe u, v, v3, vxx, chk, one, d;
+// -P from its encoding in two phases (the keyed latency kernel runs them on
+// either side of a block barrier): phase a forms y, u = y^2 - 1, v = d y^2 + 1,
+// z = u v^7 and the first half of z's (p-5)/8 power chain (z^(2^50-1),
+// z^(2^100-1)); phase b finishes the chain and the square-root checks.  The
+// operations and their order are exactly fe_pow22523's.
+struct NegDecode {
+  fe Y, u, v, v3, z, a, b;
+};
+
+PV_HD void neg_decode_a(NegDecode& st, const uint32_t s[8]) {
+  fe one, d;
   fe_const_d(d);
   fe_1(one);
-  fe_frombytes_w(h.Y, s);
+  fe_frombytes_w(st.Y, s);
+  fe_sq(st.u, st.Y);
+  fe_mul(st.v, st.u, d);
+  fe_sub(st.u, st.u, one);
+  fe_carry(st.u);              // y^2 - 1, TIGHT
+  fe_add(st.v, st.v, one);     // d y^2 + 1, LOOSE
+  fe_sq(st.v3, st.v);
+  fe_mul(st.v3, st.v3, st.v);  // v^3
+  fe_sq(st.z, st.v3);
+  fe_mul(st.z, st.z, st.v);
+  fe_mul(st.z, st.z, st.u);    // u v^7
+  fe z2, z9, t, c;             // fe_pow_2_250_1, up to 2^100 - 1
+  fe_sq(z2, st.z);
+  fe_sqn(t, z2, 2);
+  fe_mul(z9, t, st.z);
+  fe_mul(c, z9, z2);           // z^11
+  fe_sq(t, c);
+  fe_mul(st.a, t, z9);                       // 2^5 - 1
+  fe_sqn(t, st.a, 5);   fe_mul(st.b, t, st.a);  // 2^10 - 1
+  fe_sqn(t, st.b, 10);  fe_mul(c, t, st.b);     // 2^20 - 1
+  fe_sqn(t, c, 20);     fe_mul(t, t, c);        // 2^40 - 1
+  fe_sqn(t, t, 10);     fe_mul(st.a, t, st.b);  // 2^50 - 1
+  fe_sqn(t, st.a, 50);  fe_mul(st.b, t, st.a);  // 2^100 - 1
+}
+
+PV_HD bool neg_decode_b(ge_p3& h, NegDecode& st, const uint32_t s[8]) {
+  fe t;
+  fe_sqn(t, st.b, 100); fe_mul(t, t, st.b);     // 2^200 - 1
+  fe_sqn(t, t, 50);     fe_mul(t, t, st.a);     // 2^250 - 1
+  fe_sqn(t, t, 2);
+  fe_mul(h.X, t, st.z);        // z^((p-5)/8)
+  fe_copy(h.Y, st.Y);
   fe_1(h.Z);
-  fe_sq(u, h.Y);
-  fe_mul(v, u, d);
-  fe_sub(u, u, one);
-  fe_carry(u);                 // y^2 - 1, TIGHT
-  fe_add(v, v, one);           // d y^2 + 1, LOOSE
-  fe_sq(v3, v);
-  fe_mul(v3, v3, v);           // v^3
-  fe_sq(h.X, v3);
-  fe_mul(h.X, h.X, v);
-  fe_mul(h.X, h.X, u);         // u v^7
-  fe_pow22523(h.X, h.X);
-  fe_mul(h.X, h.X, v3);
-  fe_mul(h.X, h.X, u);         // u v^3 (u v^7)^((p-5)/8)
+  fe vxx, chk;
+  fe_mul(h.X, h.X, st.v3);
+  fe_mul(h.X, h.X, st.u);      // u v^3 (u v^7)^((p-5)/8)
   fe_sq(vxx, h.X);
-  fe_mul(vxx, vxx, v);
-  fe_sub(chk, vxx, u);
+  fe_mul(vxx, vxx, st.v);
+  fe_sub(chk, vxx, st.u);
   bool ok = true;
   if (!fe_iszero(chk)) {
-    fe_add(chk, vxx, u);
+    fe_add(chk, vxx, st.u);
     if (!fe_iszero(chk)) ok = false;
     fe sqrtm1;
     fe_const_sqrtm1(sqrtm1);
@@ -182,6 +212,12 @@ PV_HD bool ge_frombytes_negate(ge_p3& h, const uint32_t s[8]) {
   fe_cmov(h.X, h.X, nx, fe_isnegative(h.X) == sign);
   fe_mul(h.T, h.X, h.Y);
   return ok;
+}
+
+PV_HD bool ge_frombytes_negate(ge_p3& h, const uint32_t s[8]) {
+  NegDecode st;
+  neg_decode_a(st, s);
+  return neg_decode_b(h, st, s);
 }
 
 // canonical encoding of a p2 point as 8 LE words (y | sign(x) << 255)

@@ -848,16 +848,20 @@ hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* 
 }
 
 // k_verify_quad_keyed: the latency verdict of signatures whose key is
-// prepared (pv_quad.h q_keyed_side).  A block of 128 threads takes 8
-// signatures: wave 1 (one lane per signature) runs the pre-checks, SHA-512
-// and h mod L into an LDS record while wave 0 (8 lanes per signature) decodes
-// -R; after one barrier each quad runs its half of the comb (28 doublings, 40
-// affine adds), side 1 adds -R and side 0 tests the sum for the identity.
+// prepared (pv_quad.h q_keyed_side).  A block of 192 threads takes 8
+// signatures in three waves: wave 1 (one lane per signature) runs the
+// pre-checks, SHA-512 and h mod L into an LDS record; wave 2 (one lane per
+// signature) decodes -R -- the 250-squaring square-root chain, split around the
+// block's first barrier -- and leaves it in cached form in LDS; wave 0 (8 lanes
+// per signature, two lane quads) runs the comb of h and S as soon as the record
+// is there, overlapping the second half of the decode.  After the second
+// barrier side 1 adds -R and side 0 tests the sum for the identity.
 // LIST: signature e of the launch is list[e] (host-buffer calls whose batch
 // mixes cached and uncached keys); else e itself, and the verdict bits also
 // go to the bitmap as the block's byte.
+constexpr int KQ_NR = 41;   // -R cached in add order (Y-X, Y+X, 2dT, 2Z) + decode verdict
 template <bool LIST>
-__global__ __launch_bounds__(128) void k_verify_quad_keyed(const uint8_t* __restrict__ pk, int pk_by_key,
+__global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __restrict__ pk, int pk_by_key,
                                                            const uint8_t* __restrict__ sig,
                                                            const uint8_t* __restrict__ blob,
                                                            const uint64_t* __restrict__ off, uint64_t n,
@@ -867,47 +871,72 @@ __global__ __launch_bounds__(128) void k_verify_quad_keyed(const uint8_t* __rest
                                                            const uint32_t* __restrict__ bw, uint8_t* __restrict__ verdict,
                                                            uint8_t* __restrict__ bitmap_bytes, uint64_t bitmap_len) {
   __shared__ uint32_t recs[8 * KQ_WORDS];
+  __shared__ uint32_t negr[8 * KQ_NR];
   const int t = (int)threadIdx.x;
+  const int wave = t >> 6;
   const uint64_t e0 = (uint64_t)blockIdx.x * 8;
   const int side = (t >> 2) & 1;
   const QRole q = qrole_of((uint32_t)t & 3u);
   const uint64_t e = e0 + (uint64_t)((t & 63) >> 3);
-  const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
-  const uint64_t ic = LIST ? list[ec] : ec;
-  qfe R, eR;
-  bool okR = false;
-  if (t >= 64) {
-    // wave 1: the scalar stage, lane k for signature e0 + k
-    const int k = t - 64;
+  const int k = (t & 63);                 // waves 1 and 2: lane k < 8 serves signature e0 + k
+  const uint64_t ek = e0 + (uint64_t)k;
+  const bool serve = wave != 0 && k < 8 && ek < n;
+  uint64_t j = 0;
+  if (serve) j = LIST ? list[ek] : ek;
+  NegDecode st;
+  uint32_t enc[8];
+  if (wave == 1) {
     if (k < 8) {
-      uint32_t* r = recs + KQ_WORDS * k;
-      const uint64_t ek = e0 + (uint64_t)k;
       uint32_t dig[16];
       bool pre = false;
-      uint64_t j = 0;
-      if (ek < n) {
-        j = LIST ? list[ek] : ek;
+      if (serve) {
         const uint8_t* a = pk + 32 * (pk_by_key ? (uint64_t)kidx[j] : j);
         pre = hash_one(dig, a, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
       }
-      keyed_record(r, pre, dig, sig + 64 * j);
+      keyed_record(recs + KQ_WORDS * k, pre, dig, sig + 64 * j);
     }
-  } else {
-    // wave 0: -R (both quads of a signature decode it; side 1 adds it)
-    okR = q_decode_neg(R, sig + 64 * ic, true, q);
-    q_to_cached(eR, R, q);
+  } else if (wave == 2) {
+    if (serve) {
+      load8(enc, sig + 64 * j);
+      neg_decode_a(st, enc);
+    }
   }
   __syncthreads();
-  if (t >= 64) return;
-  const uint32_t* r = recs + KQ_WORDS * (t >> 3);
+  qfe acc;
+  const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
+  const uint64_t ic = LIST ? list[ec] : ec;
   const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
-  qfe acc, x, x1;
-  q_keyed_side(acc, eR, r, side, kt, bw, q);
+  const uint32_t* r = recs + KQ_WORDS * ((t & 63) >> 3);
+  if (wave == 0) {
+    q_comb_side(acc, r, side, kt, bw, q);
+  } else if (wave == 2 && k < 8) {
+    uint32_t* o = negr + KQ_NR * k;
+    bool ok = false;
+    ge_p3 P;
+    if (serve) ok = neg_decode_b(P, st, enc) && y_is_canonical(enc);
+    else ge_p3_0(P);
+    ge_cached c;
+    ge_p3_to_cached(c, P);
+    fe_carry(c.YmX);
+    fe_carry(c.YpX);
+    fe_carry(c.Z2);
+    store_fe(o, c.YmX);
+    store_fe(o + 10, c.YpX);
+    store_fe(o + 20, c.T2d);
+    store_fe(o + 30, c.Z2);
+    o[40] = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const uint32_t* nr = negr + KQ_NR * ((t & 63) >> 3);
+  qfe eR, x, x1;
+  q_load_cached(eR, nr, false, q);
+  q_keyed_add_negr(acc, eR, side, q);
   q_to_cached(x, acc, q);
 #pragma unroll
-  for (int k = 0; k < 10; ++k) x1.l[0].v[k] = __shfl_xor(x.l[0].v[k], 4, 64);   // side 1 -> side 0
+  for (int i = 0; i < 10; ++i) x1.l[0].v[i] = __shfl_xor(x.l[0].v[i], 4, 64);   // side 1 -> side 0
   const bool id = q_sum_is_identity(acc, x1, q);
-  const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && okR && id;
+  const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && nr[40] != 0 && id;
   const bool mine = side == 0 && (t & 3) == 0 && e < n;
   if (mine) verdict[ic] = v ? 1 : 0;
   if constexpr (!LIST) {
@@ -915,7 +944,7 @@ __global__ __launch_bounds__(128) void k_verify_quad_keyed(const uint8_t* __rest
     if (t == 0 && bitmap_bytes) {
       uint32_t bits = 0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) bits |= (uint32_t)((ball >> (8 * k)) & 1ull) << k;
+      for (int i = 0; i < 8; ++i) bits |= (uint32_t)((ball >> (8 * i)) & 1ull) << i;
       bitmap_bytes[blockIdx.x] = (uint8_t)bits;
       if ((uint64_t)blockIdx.x + 1 == gridDim.x)
         for (uint64_t b = (uint64_t)blockIdx.x + 1; b < bitmap_len; ++b) bitmap_bytes[b] = 0;
@@ -933,10 +962,10 @@ hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uin
   if (list && bitmap) return hipErrorInvalidValue;
   const uint64_t bytes = (n + 63) / 64 * 8;
   if (list)
-    hipLaunchKernelGGL(k_verify_quad_keyed<true>, dim3((uint32_t)blocks), dim3(128), 0, s, pk, pk_by_key ? 1 : 0, sig,
+    hipLaunchKernelGGL(k_verify_quad_keyed<true>, dim3((uint32_t)blocks), dim3(192), 0, s, pk, pk_by_key ? 1 : 0, sig,
                        blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0);
   else
-    hipLaunchKernelGGL(k_verify_quad_keyed<false>, dim3((uint32_t)blocks), dim3(128), 0, s, pk, pk_by_key ? 1 : 0,
+    hipLaunchKernelGGL(k_verify_quad_keyed<false>, dim3((uint32_t)blocks), dim3(192), 0, s, pk, pk_by_key ? 1 : 0,
                        sig, blob, off, n, nullptr, ktab, kidx, bw, verdict, reinterpret_cast<uint8_t*>(bitmap), bytes);
   return hipGetLastError();
 }

@@ -485,12 +485,9 @@ PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* 
   }
 }
 
-// side's point of the keyed verdict: its comb share, plus -R on side 1
-// (eR = -R in cached add order; side 0 adds the identity: the same
-// instruction stream on both quads)
-PV_HD void q_keyed_side(qfe& acc, const qfe& eR, const uint32_t* rec, int side, const uint32_t* kt,
-                        const uint32_t* bw, const QRole& q) {
-  q_comb_side(acc, rec, side, kt, bw, q);
+// side 1 adds -R (eR: -R in cached add order, q_load_cached); side 0 adds
+// the identity: the same instruction stream on both quads
+PV_HD void q_keyed_add_negr(qfe& acc, const qfe& eR, int side, const QRole& q) {
   const uint32_t sm = 0u - (uint32_t)(side != 0);
   qfe e;
 #pragma unroll
@@ -501,6 +498,25 @@ PV_HD void q_keyed_side(qfe& acc, const qfe& eR, const uint32_t* rec, int side, 
     for (int i = 0; i < 10; ++i) e.l[j].v[i] = bitsel(sm, eR.l[j].v[i], id.v[i]);
   }
   q_add(acc, e, false, q);
+}
+
+// -R of the keyed verdict as k_verify_quad_keyed's decoding lane leaves it:
+// 40 words in cached add order + the decode verdict (canonical y, on the curve)
+PV_HD void keyed_neg_r(uint32_t* o, const uint8_t* sig) {
+  uint32_t enc[8];
+  load8(enc, sig);
+  ge_p3 P;
+  const bool ok = ge_frombytes_negate(P, enc) && y_is_canonical(enc);
+  ge_cached c;
+  ge_p3_to_cached(c, P);
+  fe_carry(c.YmX);
+  fe_carry(c.YpX);
+  fe_carry(c.Z2);
+  store_fe(o, c.YmX);
+  store_fe(o + 10, c.YpX);
+  store_fe(o + 20, c.T2d);
+  store_fe(o + 30, c.Z2);
+  o[40] = ok ? 1u : 0u;
 }
 
 }  // namespace pv

@@ -267,14 +267,17 @@ void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
     uint32_t dig[16], rec[KQ_WORDS];
     const bool pre = hash_one(dig, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
     keyed_record(rec, pre, dig, sig + 64 * i);
-    qfe R, eR, Q0, Q1, x1;
-    const bool okR = q_decode_neg(R, sig + 64 * i, true, qr);
-    q_to_cached(eR, R, qr);
+    uint32_t nr[41];
+    keyed_neg_r(nr, sig + 64 * i);
+    qfe eR, Q0, Q1, x1;
+    q_load_cached(eR, nr, false, qr);
     const uint32_t* kt = ktab + (uint64_t)kidx[i] * KEY_WORDS;
-    q_keyed_side(Q0, eR, rec, 0, kt, g_bw, qr);
-    q_keyed_side(Q1, eR, rec, 1, kt, g_bw, qr);
+    q_comb_side(Q0, rec, 0, kt, g_bw, qr);
+    q_comb_side(Q1, rec, 1, kt, g_bw, qr);
+    q_keyed_add_negr(Q0, eR, 0, qr);
+    q_keyed_add_negr(Q1, eR, 1, qr);
     q_to_cached(x1, Q1, qr);
-    verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && okR && q_sum_is_identity(Q0, x1, qr)) ? 1 : 0;
+    verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && nr[40] && q_sum_is_identity(Q0, x1, qr)) ? 1 : 0;
   }
   free(ktab);
 }
