@@ -893,7 +893,7 @@ __global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __rest
         const uint8_t* a = pk + 32 * (pk_by_key ? (uint64_t)kidx[j] : j);
         pre = hash_one(dig, a, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
       }
-      keyed_record(recs + KQ_WORDS * k, pre, dig, sig + 64 * j);
+      keyed_record(recs + KQ_WORDS * k, pre, dig);
     }
   } else if (wave == 2) {
     if (serve) {
@@ -901,14 +901,15 @@ __global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __rest
       neg_decode_a(st, enc);
     }
   }
-  __syncthreads();
-  qfe acc;
   const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
   const uint64_t ic = LIST ? list[ec] : ec;
+  qfe acc, e_hi, e_lo;
+  if (wave == 0) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
+  __syncthreads();
   const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
   const uint32_t* r = recs + KQ_WORDS * ((t & 63) >> 3);
   if (wave == 0) {
-    q_comb_side(acc, r, side, kt, bw, q);
+    q_comb_side(acc, r, side, kt, e_hi, e_lo, q);
   } else if (wave == 2 && k < 8) {
     uint32_t* o = negr + KQ_NR * k;
     bool ok = false;

@@ -416,61 +416,77 @@ PV_HD bool q_sum_is_identity(const qfe& Q0, const qfe& e1, const QRole& q) {
 // test of the half-size path, pv_lattice.h): -R is decoded while the scalar
 // wave hashes, side 1 adds it, and side 0 tests Q0 + Q1 = O.
 //
-// record (LDS): h + the radix-16 digit offsets (8 words), S + the radix-2^16
-// digit offsets (8 words), pre-check verdict
-constexpr int KQ_H = 0, KQ_S = 8, KQ_OK = 16, KQ_WORDS = 17;
+// record (LDS): h + the radix-16 digit offsets (8 words), pre-check verdict
+constexpr int KQ_H = 0, KQ_OK = 8, KQ_WORDS = 9;
 
-PV_HD void keyed_record(uint32_t* rec, bool pre, const uint32_t dig[16], const uint8_t* sig) {
-  uint32_t hh[8], S[8];
+PV_HD void keyed_record(uint32_t* rec, bool pre, const uint32_t dig[16]) {
+  uint32_t hh[8];
   if (pre) {
     sc_reduce64(hh, dig);            // h = SHA-512(R||A||M) mod L (App. C.2 step 5)
-    load8(S, sig + 32);
   } else {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) hh[k] = S[k] = 0;
+    for (int k = 0; k < 8; ++k) hh[k] = 0;
   }
   sc_add_pattern(hh, hh, 0x88888888u);
-  sc_add_pattern(S, S, HALF_S_PATTERN);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    rec[KQ_H + k] = hh[k];
-    rec[KQ_S + k] = S[k];
-  }
+  for (int k = 0; k < 8; ++k) rec[KQ_H + k] = hh[k];
   rec[KQ_OK] = pre ? 1u : 0u;
 }
 
-// side's share of the comb: kt = the key's comb tables, bw = the chunk tables
-// of B.  Each window's entries (4 key, and on windows 4 and 0 four base-point
-// entries) are fetched before its four doublings.
-PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* kt, const uint32_t* bw,
-                       const QRole& q) {
-  uint32_t hp[4], sp[4];
+// S's share of the comb, which needs no hash: with the signed radix-2^16
+// digits of S (offset form), side s sums its chunks q = 4s .. 4s + 3 of the
+// high halves (added at window 4, i.e. doubled 16 times) and of the low halves
+// (added last) into two points, returned in cached add order.  Runs while the
+// scalar wave hashes.
+PV_HD void q_comb_base(qfe& e_hi, qfe& e_lo, const uint8_t* sig, int side, const uint32_t* bw, const QRole& q) {
+  uint32_t sp[8];
+  load8(sp, sig + 32);
+  sc_add_pattern(sp, sp, HALF_S_PATTERN);
+  const uint32_t* bws = bw + (uint64_t)(4 * side) * BW_TABLE;
+  qfe ph, pl, eh[4], el[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    hp[k] = rec[KQ_H + 4 * side + k];
-    sp[k] = rec[KQ_S + 4 * side + k];
+    const uint32_t wd = pick8(sp, 4 * side + k);
+    const int dh = (int)(wd >> 16) - 32768, dl = (int)(wd & 0xffffu) - 32768;
+    const uint32_t* t = bws + (uint64_t)k * BW_TABLE;
+    q_load_niels(eh[k], t + (uint64_t)(dh < 0 ? -dh : dh) * BT_WORDS, dh < 0, q);
+    q_load_niels(el[k], t + (uint64_t)(dl < 0 ? -dl : dl) * BT_WORDS, dl < 0, q);
   }
+#pragma unroll
+  for (int j = 0; j < QL; ++j) {
+    role_p3_identity(ph.l[j], qrole(j, q));
+    role_p3_identity(pl.l[j], qrole(j, q));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t wd = pick8(sp, 4 * side + k);
+    q_add(ph, eh[k], (wd >> 16) < 32768u, q);
+    q_add(pl, el[k], (wd & 0xffffu) < 32768u, q);
+  }
+  q_to_cached(e_hi, ph, q);
+  q_to_cached(e_lo, pl, q);
+}
+
+// h's share of the comb on side s: the key tables q = 4s .. 4s + 3 (kt = the
+// key's 8 comb tables), 8 windows of 4 doublings; the base-point sums of
+// q_comb_base join at window 4 (e_hi) and after the last window (e_lo).  Each
+// window's 4 key entries are fetched before its doublings.
+PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* kt, const qfe& e_hi, const qfe& e_lo,
+                       const QRole& q) {
+  uint32_t hp[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hp[k] = rec[KQ_H + 4 * side + k];
   const uint32_t* kts = kt + 4 * side * KT_TABLE;
-  const uint32_t* bws = bw + (uint64_t)(4 * side) * BW_TABLE;
 #pragma unroll
   for (int j = 0; j < QL; ++j) role_p3_identity(acc.l[j], qrole(j, q));
 #pragma unroll 1
   for (int w = 7; w >= 0; --w) {
-    qfe ek[4], eb[4];
-    int dk[4], db[4];
+    qfe ek[4];
+    int dk[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       dk[k] = (int)((hp[k] >> (4 * w)) & 15u) - 8;
       q_load_niels(ek[k], kts + k * KT_TABLE + (dk[k] < 0 ? -dk[k] : dk[k]) * KT_ENTRY, dk[k] < 0, q);
-    }
-    const bool bwin = (w & 3) == 0;
-    if (bwin) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        db[k] = (int)((sp[k] >> (4 * w)) & 0xffffu) - 32768;   // w = 4: high halves, w = 0: low
-        q_load_niels(eb[k], bws + (uint64_t)k * BW_TABLE + (uint64_t)(db[k] < 0 ? -db[k] : db[k]) * BT_WORDS,
-                     db[k] < 0, q);
-      }
     }
     if (w != 7) {
 #pragma unroll 1
@@ -478,11 +494,9 @@ PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* 
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) q_add(acc, ek[k], dk[k] < 0, q);
-    if (bwin) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) q_add(acc, eb[k], db[k] < 0, q);
-    }
+    if (w == 4) q_add(acc, e_hi, false, q);
   }
+  q_add(acc, e_lo, false, q);
 }
 
 // side 1 adds -R (eR: -R in cached add order, q_load_cached); side 0 adds

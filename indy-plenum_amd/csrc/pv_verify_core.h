@@ -610,6 +610,30 @@ PV_HD void store_xyz(uint32_t* p, const ge_p3& q) {
   store_fe(p + 20, q.Z);
 }
 
+// one 32-word affine entry (a, b, c at words 0, 10, 20; words 30-31 zero) as
+// eight 16-byte stores: the table is key-major, so each store instruction of a
+// wave touches 64 cache lines -- 8 wide stores instead of 30 narrow ones
+PV_HD void store_entry32(uint32_t* slot, const fe& a, const fe& b, const fe& c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t w[32];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    w[i] = a.v[i];
+    w[10 + i] = b.v[i];
+    w[20 + i] = c.v[i];
+  }
+  w[30] = w[31] = 0;
+  uint4* d = reinterpret_cast<uint4*>(slot);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+#else
+  store_fe(slot, a);
+  store_fe(slot + 10, b);
+  store_fe(slot + 20, c);
+  slot[30] = slot[31] = 0;
+#endif
+}
+
 // kt: KEY_WORDS words (key-major); scr: KEY_SCRATCH words of this key's
 // scratch, word w at scr[w * LS] (LS = 64 on the device: lane-interleaved)
 template <int LS = 1>
@@ -700,24 +724,19 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
     }
     fe_mul(x, x, zi);
     fe_mul(y, y, zi);
-    fe_add(u, y, x); fe_carry(u);
-    store_fe(slot, u);
-    fe_sub(u, y, x); fe_carry(u);
-    store_fe(slot + 10, u);
+    fe ypx, ymx;
+    fe_add(ypx, y, x); fe_carry(ypx);
+    fe_sub(ymx, y, x); fe_carry(ymx);
     fe_mul(u, x, y);
     fe_mul(u, u, d2);
-    store_fe(slot + 20, u);
+    store_entry32(slot, ypx, ymx, u);
   }
   // identity entries (k = 0): y+x = 1, y-x = 1, 2dxy = 0
   fe one, zero;
   fe_1(one);
   fe_0(zero);
 #pragma unroll 1
-  for (int q = 0; q < COMB_Q; ++q) {
-    store_fe(kt + q * KT_TABLE, one);
-    store_fe(kt + q * KT_TABLE + 10, one);
-    store_fe(kt + q * KT_TABLE + 20, zero);
-  }
+  for (int q = 0; q < COMB_Q; ++q) store_entry32(kt + q * KT_TABLE, one, one, zero);
 }
 
 // R' = hh*(-A) + ss*B from a prepared key (8 comb tables in kt) and the eight

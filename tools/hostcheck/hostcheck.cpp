@@ -266,14 +266,17 @@ void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
   for (uint64_t i = 0; i < n; ++i) {
     uint32_t dig[16], rec[KQ_WORDS];
     const bool pre = hash_one(dig, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
-    keyed_record(rec, pre, dig, sig + 64 * i);
+    keyed_record(rec, pre, dig);
     uint32_t nr[41];
     keyed_neg_r(nr, sig + 64 * i);
     qfe eR, Q0, Q1, x1;
     q_load_cached(eR, nr, false, qr);
     const uint32_t* kt = ktab + (uint64_t)kidx[i] * KEY_WORDS;
-    q_comb_side(Q0, rec, 0, kt, g_bw, qr);
-    q_comb_side(Q1, rec, 1, kt, g_bw, qr);
+    qfe h0, l0, h1, l1;
+    q_comb_base(h0, l0, sig + 64 * i, 0, g_bw, qr);
+    q_comb_base(h1, l1, sig + 64 * i, 1, g_bw, qr);
+    q_comb_side(Q0, rec, 0, kt, h0, l0, qr);
+    q_comb_side(Q1, rec, 1, kt, h1, l1, qr);
     q_keyed_add_negr(Q0, eR, 0, qr);
     q_keyed_add_negr(Q1, eR, 1, qr);
     q_to_cached(x1, Q1, qr);
