@@ -43,19 +43,24 @@ static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS
 // ------------------------------------------------------------- hash kernel
 // Persistent lanes with per-lane refill: each lane runs ONE SHA-512
 // compression of its current message per loop trip and, when that message is
-// done, stores the digest and takes the next message index from a global
-// counter (one atomic per wavefront).  Ragged message lengths (C4: 2..33
-// blocks) then cost no SIMD divergence: a lane never waits for a longer
-// message in its wavefront, only the final drain is ragged.
-__device__ __forceinline__ uint64_t take_index(unsigned long long* counter) {
-  const uint64_t active = __ballot(1);
-  const int lane = (int)(threadIdx.x & 63u);
-  const int leader = __ffsll((unsigned long long)active) - 1;
-  const uint32_t rank = (uint32_t)__popcll(active & ((1ull << lane) - 1ull));
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(active));
-  base = __shfl(base, leader, 64);
-  return (uint64_t)base + rank;
+// done, stores the digest and takes the next message index from a
+// wave-private chunk of the global queue (wq_take below).  Ragged message
+// lengths (C4: 2..33 blocks) then cost no SIMD divergence: a lane never waits
+// for a longer message in its wavefront, only the final drain is ragged.
+__device__ __forceinline__ uint64_t readlane64(unsigned long long v, int lane) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+}
+
+// Base index of a wave's __popcll(m) entries appended at *counter (m = the
+// wave's nonzero ballot; call with the whole wavefront active): the first
+// set lane adds, every lane reads its result with v_readlane at that
+// (uniform) lane index -- no cross-lane shuffle through LDS.
+__device__ __forceinline__ uint64_t wave_append(unsigned long long* counter, uint64_t m) {
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  unsigned long long b = 0;
+  if ((int)(threadIdx.x & 63u) == leader) b = atomicAdd(counter, (unsigned long long)__popcll(m));
+  return readlane64(b, leader);
 }
 
 // Wave-private chunks of the global message queue: the wave takes CH indices
@@ -419,10 +424,7 @@ __global__ __launch_bounds__(256) void k_lattice(const uint8_t* __restrict__ pk,
   const uint64_t m = __ballot(defer);
   if (m) {
     const int lane = (int)(threadIdx.x & 63u);
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(dcount, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader, 64);
+    const uint64_t base = wave_append(dcount, m);
     if (defer) dlist[base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
   }
 }
@@ -753,10 +755,7 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_chunk_half(
     const bool defer = st == HS_DEFER;
     const uint64_t m = __ballot(defer);
     if (m) {
-      const int leader = __ffsll((unsigned long long)m) - 1;
-      unsigned long long b = 0;
-      if (lane == leader) b = atomicAdd(dcount, (unsigned long long)__popcll(m));
-      b = __shfl(b, leader, 64);
+      const uint64_t b = wave_append(dcount, m);
       if (defer) dlist[b + (uint64_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(base + i);
     }
     bool ok = false;

@@ -24,6 +24,15 @@ def main():
         for dedup in (True, False):
             got = nat.verify_batch_arrays(r['pk'], r['sig'], r['blob'], r['off'], device_mask=mask, dedup_keys=dedup)
             out['golden_mask{}_dedup{}'.format(mask, int(dedup))] = bool((got == want).all())
+    # the persistent key cache on both engine devices: every golden key cached,
+    # shards of Looper-pass size (mask 0b11 splits 1,000 signatures 500 / 500)
+    nat.keycache_add(r['pk'])
+    for n_small in (1, 1000, 3000):
+        o = r['off'][:n_small + 1]
+        got = nat.verify_batch_arrays(r['pk'][:n_small], r['sig'][:n_small], r['blob'][:int(o[-1])], o,
+                                      device_mask=0b11)
+        out['keycache_{}'.format(n_small)] = bool((got == want[:n_small]).all())
+    nat.keycache_clear()
     # a C4-shaped batch: 300k signatures, 128 B - 4 KB messages, a pool of 4096
     # keys (the dedup flag takes the keyed path), 5 % tampered
     rng = np.random.default_rng(44)

@@ -20,8 +20,9 @@ def test_two_engine_devices_shard_and_fail_per_shard():
     assert p.returncode == 0, p.stderr[-3000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out['devices'] == 2, out
+    assert {'keycache_1', 'keycache_1000', 'keycache_3000'} <= set(out), out
     for k, v in out.items():
-        if k.startswith(('golden_', 'c4_')) or k == 'after_errors':
+        if k.startswith(('golden_', 'c4_', 'keycache_')) or k == 'after_errors':
             assert v is True, (k, out)
     assert out['shard_error'] and 'device 1' in out['shard_error'] and 'not monotone' in out['shard_error'], out
     assert out['boundary_error'] and 'shard 1' in out['boundary_error'], out
