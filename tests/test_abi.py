@@ -73,6 +73,18 @@ def test_fails_loudly_without_gpu(native):
     with pytest.raises(native.PlenumGpuError):
         native.verify_batch_arrays(np.zeros((1, 32), np.uint8), np.zeros((1, 64), np.uint8),
                                    np.zeros(0, np.uint8), np.zeros(2, np.uint64))
+    # the key cache: nothing to prepare it on
+    assert lib.pv_keycache_add(p(buf), 1) == -77   # PV_ENOTINIT
+    c = ctypes.c_uint64(5)
+    assert lib.pv_keycache_size(ctypes.byref(c)) == 0 and c.value == 0
+    assert lib.pv_keycache_clear() == 0
+    # keys registered without a GPU are only queued (SimpleAuthNr.addIdr must not raise)
+    from plenum_gpu.client_authn import SimpleAuthNr
+    from plenum_gpu import base58
+    SimpleAuthNr().addIdr('did', base58.b58encode(bytes(range(32))).decode())
+    assert native._pending_keys
+    native.keycache_clear()
+    assert not native._pending_keys
 
 
 def test_no_cpu_fallback_in_product_package():
