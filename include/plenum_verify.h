@@ -304,13 +304,9 @@ int pv_set_lat_keyed_max(uint64_t max_signatures);
 int pv_set_lat_kernel(uint32_t kernel);
 /* Host-buffer chunks of generic batches above the latency size: 1 (default) =
  * one fused launch per chunk (pre-checks + hash + scalar stage + half-size
- * curve per 64-signature task) except the last chunk, which runs the
- * device-resident schedule (its deferred records are full-length tasks of its
- * own curve grid) while the earlier chunks' deferred records take a lane-quad
- * pass on the other stream; 2 = every chunk fused and one lane-quad pass over
- * all deferred records after the last; 0 = the device-resident schedule (hash,
- * lattice, curve launches) per chunk.  Same verdicts.  Env PV_HOST_FUSED=0|1|2
- * at pv_init. */
+ * curve per 64-signature task) and one lane-quad pass over the deferred
+ * records; 0 = the device-resident schedule (hash, lattice, curve launches)
+ * per chunk.  Same verdicts.  Env PV_HOST_FUSED=0|1 at pv_init. */
 int pv_set_host_fused(int enable);
 int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 

@@ -414,12 +414,6 @@ struct Device {
   // + one k_verify_quad_list pass for the deferred records; PV_HOST_FUSED=0:
   // k_hash + k_lattice + k_curve_half per chunk (the device-resident schedule)
   bool chunk_fused = true;
-  // the LAST chunk of a fused host call runs the device-resident schedule
-  // (hash, lattice, curve with its own full-length tasks) while the earlier
-  // chunks' deferred records take their lane-quad pass on the other stream:
-  // no deferred pass after the last grid (PV_HOST_FUSED=1; 2 = fused last chunk
-  // + one deferred pass at the end)
-  bool last_unfused = true;
   DevBuf<uint32_t> dl;               // shard indices deferred by k_chunk_half
   DevBuf<unsigned long long> dlc;    // their count
   hipEvent_t joined = nullptr;       // ws[1] drained into ws[0] (deferred pass)
@@ -534,10 +528,8 @@ int init_device(Device& d) {
   }
   d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped;
   if (const char* t = getenv("PV_HOST_FUSED")) {
-    if (strcmp(t, "0") != 0 && strcmp(t, "1") != 0 && strcmp(t, "2") != 0)
-      return fail(PV_EINVAL, "PV_HOST_FUSED must be 0, 1 or 2 (got %s)", t);
-    d.chunk_fused = t[0] != '0';
-    d.last_unfused = t[0] == '1';
+    if (strcmp(t, "0") != 0 && strcmp(t, "1") != 0) return fail(PV_EINVAL, "PV_HOST_FUSED must be 0 or 1 (got %s)", t);
+    d.chunk_fused = t[0] == '1';
   }
   if (const char* m = getenv("PV_LAT_KERNEL")) {
     if (!strcmp(m, "pair")) d.lat_quad = false;
@@ -1151,26 +1143,6 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     HIP_OK(hipEventRecord(d.copied, d.copy));
     HIP_OK(hipStreamWaitEvent(w.stream, d.copied, 0));
     // blob base + shard-relative offsets: the hash kernel reads blob + off[i]
-    const bool last_split = fused && d.last_unfused && c + 1 == nch && nch >= 2;
-    if (last_split) {
-      // the deferred records of chunks 0 .. c - 1 (listed by their fused
-      // launches) on the other stream, after both streams' earlier chunks ...
-      Workspace& o = d.ws[(c + 1) & 1];
-      HIP_OK(hipEventRecord(d.joined, w.stream));
-      HIP_OK(hipStreamWaitEvent(o.stream, d.joined, 0));
-      HIP_OK(pv::launch_verify_quad_list(d.pk.p, d.sig.p, d.blob.p, d.off.p, d.dl.p, d.dlc.p, c0, d.cu_count * 8,
-                                         d.bw.p, d.verdict.p, d.mode == CurveMode::Full, o.stream));
-      if (const int rc = ws_end(o, o.stream)) return rc;
-      // ... while this chunk runs hash, lattice and the half-size curve kernel,
-      // whose full-length tasks verify its own deferred records first
-      int rc = enqueue_verify(d, w, d.pk.p + 32 * c0, d.sig.p + 64 * c0, d.blob.p, d.off.p + c0, mc, d.verdict.p + c0,
-                              nullptr, w.stream, false, nullptr, nullptr);
-      if (rc) return rc;
-      if (trace)
-        fprintf(stderr, "[pv host] chunk %zu (%llu sigs, device schedule): begin %.1f slot-free %.1f gathered %.1f "
-                "enqueued %.1f us\n", c, (unsigned long long)mc, t_begin, t_slot, t_gather, us());
-      continue;
-    }
     if (fused) {
       HIP_OK(w.hrec.ensure(mc * pv::HSREC_WORDS));
       HIP_OK(w.qc.ensure(2));
@@ -1196,15 +1168,13 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   }
   if (fused) {
     // the deferred records of every chunk (ws[1]'s chunks joined into ws[0]),
-    // unless the last chunk already split them off; then all verdicts in one copy
+    // then all verdicts in one copy
     Workspace& w0 = d.ws[0];
     HIP_OK(hipEventRecord(d.joined, d.ws[1].stream));
     HIP_OK(hipStreamWaitEvent(w0.stream, d.joined, 0));
-    if (!(d.last_unfused && nch >= 2))
-      HIP_OK(pv::launch_verify_quad_list(d.pk.p, d.sig.p, d.blob.p, d.off.p, d.dl.p, d.dlc.p, m, d.cu_count * 8,
-                                         d.bw.p, d.verdict.p, d.mode == CurveMode::Full, w0.stream));
+    HIP_OK(pv::launch_verify_quad_list(d.pk.p, d.sig.p, d.blob.p, d.off.p, d.dl.p, d.dlc.p, m, d.cu_count * 8, d.bw.p,
+                                       d.verdict.p, d.mode == CurveMode::Full, w0.stream));
     HIP_OK(hipMemcpyAsync(pinned ? d.vout.p : hb.verdict + s, d.verdict.p, m, hipMemcpyDeviceToHost, w0.stream));
-    for (auto& w : d.ws) w.half_ran = false;   // pv_curve_stats describes device-resident calls
   }
   HIP_OK(hipStreamSynchronize(d.copy));
   for (auto& w : d.ws) HIP_OK(hipStreamSynchronize(w.stream));
@@ -1593,11 +1563,7 @@ int pv_set_curve_mode(uint32_t mode) {
 int pv_set_host_fused(int enable) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
-  if (enable < 0 || enable > 2) return fail(PV_EINVAL, "enable must be 0, 1 or 2");
-  for (auto& d : g_devs) {
-    d.chunk_fused = enable != 0;
-    d.last_unfused = enable == 1;
-  }
+  for (auto& d : g_devs) d.chunk_fused = enable != 0;
   return PV_OK;
 }
 

@@ -183,11 +183,9 @@ def set_lat_kernel(name):
 
 
 def set_host_fused(enable):
-    """Host-buffer chunks (pv_set_host_fused): True / 1 (default) = one fused
-    launch per chunk, the last chunk on the device-resident schedule beside the
-    earlier chunks' deferred pass; 2 = every chunk fused + one deferred pass at
-    the end; False / 0 = the hash / lattice / curve launches per chunk."""
-    _check('pv_set_host_fused', load().pv_set_host_fused(int(enable)))
+    """Host-buffer chunks: one fused launch per chunk + a deferred pass (True,
+    default) or the hash / lattice / curve launches per chunk (pv_set_host_fused)."""
+    _check('pv_set_host_fused', load().pv_set_host_fused(1 if enable else 0))
 
 
 STAGING_MODES = {0: 'pinned', 1: 'pageable'}   # PV_STAGING_PINNED / _PAGEABLE
