@@ -335,6 +335,8 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
   // prepared keys reads the radix-2^16 chunk tables bw from L2/MALL
   constexpr int TW = BTAB_ENTRIES * BTAB_WORDS;
   __shared__ uint32_t btab[KEYED ? 1 : TW];
+  // keyed: the comb's 16 digit words per lane, lane-interleaved
+  __shared__ uint32_t dg[KEYED ? 16 * CURVE_BLOCK : 1];
   if constexpr (!KEYED) {
     for (int j = threadIdx.x; j < TW; j += CURVE_BLOCK) btab[j] = btab_g[j];
     __syncthreads();
@@ -353,7 +355,8 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
     const uint64_t t = wave_task(tasks);
     if (t >= ntasks) break;
     const uint64_t i0 = t * PER + (uint64_t)ln;
-    const uint32_t okm = curve_group<KEYED>(pk, sig, hin, pre, i0, 64, n, lane, btab, ktab, kidx, bw);
+    const uint32_t okm = curve_group<KEYED, KEYED ? CURVE_BLOCK : 1>(pk, sig, hin, pre, i0, 64, n, lane, btab, ktab,
+                                                                      kidx, bw, dg + threadIdx.x);
 #pragma unroll
     for (int k = 0; k < CURVE_K; ++k) {
       const uint64_t i = i0 + 64ull * (uint64_t)k;

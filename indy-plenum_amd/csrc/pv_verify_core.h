@@ -18,9 +18,6 @@ namespace pv {
 
 constexpr int BT_ENTRIES = 129;   // niels k*B, k = 0..128
 constexpr int BT_WORDS = 32;      // 3 fe (30 words) padded to 32
-#ifndef PV_COMB_PREFETCH
-#define PV_COMB_PREFETCH 1
-#endif
 #ifndef PV_HALF_PREFETCH
 #define PV_HALF_PREFETCH 1
 #endif
@@ -747,20 +744,31 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
 // radix 256 needed 32).  Every table entry is fetched one add ahead into
 // ping-pong registers.  The chunk loops are not unrolled (code size); the
 // digit words rotate through static indices.
+//
+// The 16 offset digit words (h, S) live in `dg` (word k at dg[k * DS]): the
+// kernel passes a lane-interleaved LDS array (DS = the block size), so they
+// hold no registers through the comb (the keyed kernel sits at 256 VGPRs);
+// DS = 1 is a plain local array (host build).
+template <int DS = 1>
 PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32_t ss[8], const uint32_t* kt,
-                                  const uint32_t* bw) {
-  uint32_t hp[8], sp[8];
-  sc_add_pattern(hp, hh, 0x88888888u);
-  sc_add_pattern(sp, ss, HALF_S_PATTERN);
+                                  const uint32_t* bw, uint32_t* dg) {
+  {
+    uint32_t hp[8], sp[8];
+    sc_add_pattern(hp, hh, 0x88888888u);
+    sc_add_pattern(sp, ss, HALF_S_PATTERN);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      dg[k * DS] = hp[k];
+      dg[(8 + k) * DS] = sp[k];
+    }
+  }
   ge_p3 acc;
   ge_p3_0(acc);
   ge_p1p1 t;
   ge_p2 r2;
-#if PV_COMB_PREFETCH
   ge_nentry ea, eb;
-  int dA = (int)((hp[0] >> 28) & 15u) - 8;
+  int dA = (int)((dg[0] >> 28) & 15u) - 8;
   load_nentry(ea, kt + (dA < 0 ? -dA : dA) * KT_ENTRY, dA < 0);
-#endif
 #pragma unroll 1
   for (int w = 7; w >= 0; --w) {
     if (w != 7) {
@@ -774,74 +782,47 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
     }
     const int sh4 = 4 * w;
     const bool bwin = (w & 3) == 0;
-#if PV_COMB_PREFETCH
     // two key adds per trip, ping-ponging the register entries: the entry of
-    // the next add (hp[1] holds its digit word; q = 0 of window w - 1 after
-    // the last one) is in flight during the current add
+    // the next add (chunk q + 1; chunk 0 of window w - 1 after the last one)
+    // is in flight during the current add
 #pragma unroll 1
     for (int q = 0; q < COMB_Q; q += 2) {
       {
-        const int dn = (int)((hp[1] >> sh4) & 15u) - 8;
+        const int dn = (int)((dg[(q + 1) * DS] >> sh4) & 15u) - 8;
         load_nentry(eb, kt + (q + 1) * KT_TABLE + (dn < 0 ? -dn : dn) * KT_ENTRY, dn < 0);
         ge_madd_entry(t, acc, ea, dA < 0);
         ge_p1p1_to_p3(acc, t);
-        const uint32_t x = hp[0];
-#pragma unroll
-        for (int j = 0; j < 7; ++j) hp[j] = hp[j + 1];
-        hp[7] = x;
         dA = dn;
       }
       {
         const bool last = q + 2 >= COMB_Q;
         const bool more = !last || w > 0;
-        const int dn = (int)((hp[1] >> ((last ? sh4 - 4 : sh4) & 31)) & 15u) - 8;
+        const int dn = (int)((dg[(last ? 0 : q + 2) * DS] >> ((last ? sh4 - 4 : sh4) & 31)) & 15u) - 8;
         if (more) load_nentry(ea, kt + (last ? 0 : q + 2) * KT_TABLE + (dn < 0 ? -dn : dn) * KT_ENTRY, dn < 0);
         ge_madd_entry(t, acc, eb, dA < 0);
         if (!last || bwin) ge_p1p1_to_p3(acc, t);
         else ge_p1p1_to_p2(r2, t);          // a doubling comes next: no T needed
-        const uint32_t x = hp[0];
-#pragma unroll
-        for (int j = 0; j < 7; ++j) hp[j] = hp[j + 1];
-        hp[7] = x;
         dA = dn;
       }
     }
-#else
-#pragma unroll 1
-    for (int q = 0; q < COMB_Q; ++q) {
-      const int dA = (int)((hp[0] >> sh4) & 15u) - 8;
-      ge_madd_at(t, acc, kt + q * KT_TABLE + (dA < 0 ? -dA : dA) * KT_ENTRY, dA < 0);
-      if (q + 1 < COMB_Q || bwin) ge_p1p1_to_p3(acc, t);
-      else ge_p1p1_to_p2(r2, t);          // a doubling comes next: no T needed
-      const uint32_t x = hp[0];
-#pragma unroll
-      for (int j = 0; j < 7; ++j) hp[j] = hp[j + 1];
-      hp[7] = x;
-    }
-#endif
     if (bwin) {
       const int sh16 = 4 * w;   // w = 4: high half of each word, w = 0: low half
       ge_nentry ba, bb;
-      int db = (int)((sp[0] >> sh16) & 0xffffu) - 32768;
+      int db = (int)((dg[8 * DS] >> sh16) & 0xffffu) - 32768;
       load_nentry(ba, bw + (db < 0 ? -db : db) * BT_WORDS, db < 0);
 #pragma unroll 1
       for (int q = 0; q < COMB_Q; q += 2) {
-        const int d1 = (int)((sp[1] >> sh16) & 0xffffu) - 32768;
+        const int d1 = (int)((dg[(8 + q + 1) * DS] >> sh16) & 0xffffu) - 32768;
         load_nentry(bb, bw + (q + 1) * BW_TABLE + (d1 < 0 ? -d1 : d1) * BT_WORDS, d1 < 0);
         ge_madd_entry(t, acc, ba, db < 0);
         ge_p1p1_to_p3(acc, t);
         const bool last = q + 2 >= COMB_Q;
-        const int d2 = (int)((sp[2] >> sh16) & 0xffffu) - 32768;
+        const int d2 = last ? 0 : (int)((dg[(8 + q + 2) * DS] >> sh16) & 0xffffu) - 32768;
         if (!last) load_nentry(ba, bw + (q + 2) * BW_TABLE + (d2 < 0 ? -d2 : d2) * BT_WORDS, d2 < 0);
         ge_madd_entry(t, acc, bb, d1 < 0);
         if (!last) ge_p1p1_to_p3(acc, t);
         else ge_p1p1_to_p2(r2, t);
         db = d2;
-        const uint32_t x0 = sp[0], x1 = sp[1];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) sp[j] = sp[j + 2];
-        sp[6] = x0;
-        sp[7] = x1;
       }
     }
   }
@@ -849,8 +830,9 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
 }
 
 // R' = h(-A) + S B with -A's comb tables taken from a prepared key
+template <int DS = 1>
 PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, const uint32_t* dig_src,
-                             const uint32_t* bw) {
+                             const uint32_t* bw, uint32_t* dg) {
   if (!kt[KEY_STATUS]) return false;
   uint32_t hh[8], S[8];
   {
@@ -860,7 +842,7 @@ PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, 
     sc_reduce64(hh, dig);
   }
   load8(S, sig + 32);
-  double_scalarmult_comb(rp, hh, S, kt, bw);
+  double_scalarmult_comb<DS>(rp, hh, S, kt, bw, dg);
   return true;
 }
 
@@ -899,11 +881,13 @@ PV_HD void batch_invert_z(uint32_t* pts, int K) {
 // shared inversion.  scratch = LANE_WORDS words owned by this lane.
 // KEYED: signature i uses prepared key kidx[i] (comb tables in ktab; btab
 // then holds the even chunk tables 0, 2, 4, 6 and bg all eight).
-template <bool KEYED>
+template <bool KEYED, int DS = 1>
 PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre, uint64_t i0,
                            uint64_t stride, uint64_t n, uint32_t* scratch, const uint32_t* btab,
                            const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr,
-                           const uint32_t* bg = nullptr) {
+                           const uint32_t* bg = nullptr, uint32_t* dg = nullptr) {
+  uint32_t dloc[DS == 1 ? 16 : 1];   // host build: the comb's digit words
+  if (DS == 1) dg = dloc;
   uint32_t* pts = scratch + AT_WORDS;
   uint32_t live = 0;
 #pragma unroll 1
@@ -913,7 +897,7 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     bool ok = false;
     if (i < n && pre[i]) {
       if constexpr (KEYED)
-        ok = curve_point_keyed(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, bg);
+        ok = curve_point_keyed<DS>(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, bg, dg);
       else
         ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);
     }
@@ -1021,14 +1005,12 @@ PV_HD uint32_t lattice_one(uint32_t* rec, bool pre, const uint32_t* dig, const u
 template <int LS = 1>
 PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const uint32_t* rtab, const uint32_t* blo,
                     const uint32_t* bhi) {
-  uint32_t cp[4], dp[4], sl[4], sh[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    cp[k] = rec[HREC_C + k];
-    dp[k] = rec[HREC_D + k];
-    sl[k] = rec[HREC_S + k];
-    sh[k] = rec[HREC_S + 4 + k];
-  }
+  // digit words: the current group (windows 8g .. 8g + 7 of |c|, d and the
+  // 16-bit digits of s' halves) in registers and the next lower group loaded
+  // one group ahead from the record -- not all 16 words live through the loop
+  // (register pressure: the kernel sits at 256 VGPRs)
+  uint32_t cw = rec[HREC_C + 3], dw = rec[HREC_D + 3], lw = rec[HREC_S + 3], hw = rec[HREC_S + 7];
+  uint32_t cn = rec[HREC_C + 2], dn = rec[HREC_D + 2], ln = rec[HREC_S + 2], hn = rec[HREC_S + 6];
   ge_p3 acc;
   ge_p2 r2;
   ge_p3_0(acc);
@@ -1040,7 +1022,6 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
     ge_add_cached_at<LS>(t, acc, rtab + (dR < 0 ? -dR : dR) * AT_ENTRY * LS, dR < 0);
     ge_p1p1_to_p2(r2, t);
   }
-  uint32_t cw = cp[3], dw = dp[3], lw = sl[3], hw = sh[3];
 #if PV_HALF_PREFETCH
   // software pipeline: the +-A entry of window w is loaded before its four
   // doublings, the -R entry before the +-A add
@@ -1051,18 +1032,18 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
 #pragma unroll 1
   for (int w = 31; w >= 0; --w) {
     if ((w & 7) == 7 && w != 31) {
-      // next lower digit word, static indices only (no scratch spill of the arrays)
-#pragma unroll
-      for (int k = 3; k > 0; --k) {
-        cp[k] = cp[k - 1];
-        dp[k] = dp[k - 1];
-        sl[k] = sl[k - 1];
-        sh[k] = sh[k - 1];
+      // next lower digit group; the one after it is fetched now
+      cw = cn;
+      dw = dn;
+      lw = ln;
+      hw = hn;
+      const int g = (w >> 3) - 1;
+      if (g >= 0) {
+        cn = rec[HREC_C + g];
+        dn = rec[HREC_D + g];
+        ln = rec[HREC_S + g];
+        hn = rec[HREC_S + 4 + g];
       }
-      cw = cp[3];
-      dw = dp[3];
-      lw = sl[3];
-      hw = sh[3];
     }
 #pragma unroll 1
     for (int k = 0; k < 3; ++k) {
@@ -1120,8 +1101,8 @@ PV_HD void msm_half(ge_p1p1& t, const uint32_t* rec, const uint32_t* atab, const
     if (w == 0) break;
 #if PV_HALF_PREFETCH
     {
-      // digit of window w - 1: its word is cp[2] when w - 1 starts a new word
-      const uint32_t nw = ((w - 1) & 7) == 7 ? cp[2] : cw;
+      // digit of window w - 1: its word is the next group's when w - 1 starts one
+      const uint32_t nw = ((w - 1) & 7) == 7 ? cn : cw;
       dA = (int)((nw >> (4 * ((w - 1) & 7))) & 15u) - 8;
       load_entry<LS>(ea, atab + (dA < 0 ? -dA : dA) * AT_ENTRY * LS, dA < 0);
     }
