@@ -529,6 +529,24 @@ def main_bls(args):
                      'note': 'W = {} Fp mul x 180 + {} sqr x 135 v_mad_i64_i32 per check (host op counts)'
                              .format(BLS_W_MUL, BLS_W_SQR)},
     }
+    # the per-COMMIT regime: host calls of 1 check, one 3PC batch (25 COMMITs,
+    # one message) and 10 batches (pv_bls_verify_batch, host buffers)
+    sig_h = sig[:250].cpu().numpy()
+    mi_h = midx[:250].cpu().numpy().astype(np.uint32)
+    ki_h = kidx[:250].cpu().numpy().astype(np.uint32)
+    lat, lat_bad = {}, 0
+    for m in (1, 25, 250):
+        vb = nat.bls_verify_arrays(sig_h[:m], blob_h, off_h[:int(mi_h[m - 1]) + 2], mi_h[:m], ki_h[:m])
+        lat_bad += int((vb != expect[:m].cpu().numpy()).sum())
+        ts = []
+        for _ in range(5):
+            t1 = time.perf_counter()
+            nat.bls_verify_arrays(sig_h[:m], blob_h, off_h[:int(mi_h[m - 1]) + 2], mi_h[:m], ki_h[:m])
+            ts.append(time.perf_counter() - t1)
+        ts.sort()
+        lat[str(m)] = {'ms_median': round(ts[2] * 1e3, 3), 'ms_min': round(ts[0] * 1e3, 3)}
+    lat['verdict_mismatches'] = lat_bad
+    out['small_batch_latency'] = lat
     if not args.no_cpu_baseline:
         orc = ctypes.CDLL(os.path.join(REPO, 'oracle', 'libbls_oracle.so'))
         sample = 2000
