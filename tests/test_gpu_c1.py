@@ -43,6 +43,14 @@ def test_c1_10k_batch_equals_per_request():
     want = [_outcome(x) for x in single]
     bad = [k for k in range(n) if got[k] != want[k]]
     assert not bad, [(k, got[k], want[k]) for k in bad[:5]]
+    # addIdr put the DIDs' keys in the device key cache, so both runs above took
+    # the keyed latency kernel; without the cache the generic kernels agree too
+    from plenum_gpu import _native as nat
+    assert nat.keycache_size() > 0.9 * n
+    nat.keycache_clear()
+    uncached = [_outcome(x) for x in authnr.authenticate_batch(reqs)]
+    bad = [k for k in range(n) if uncached[k] != want[k]]
+    assert not bad, [(k, uncached[k], want[k]) for k in bad[:5]]
     kinds = {w[0] for w in want}
     assert {'ok', 'InsufficientCorrectSignatures', 'InvalidSignatureFormat'} <= kinds, kinds
     assert all(want[k][0] != 'ok' for k in unknown)
