@@ -14,7 +14,9 @@ step c1 && timeout -k 10 240 python bench.py --config c1 > "$out/bench_c1.json" 
 step c3 && timeout -k 10 240 python bench.py --config c3 > "$out/bench_c3.json" 2> "$out/bench_c3.err" && \
 step c4 && timeout -k 10 300 python bench.py --config c4 --steps 5 --warmup 2 > "$out/bench_c4.json" 2> "$out/bench_c4.err" && \
 step f3 && timeout -k 10 240 python bench.py --config f3 > "$out/bench_f3.json" 2> "$out/bench_f3.err" && \
+step c3bls && timeout -k 10 300 python bench.py --config c3bls > "$out/bench_c3bls.json" 2> "$out/bench_c3bls.err" && \
 step latency && timeout -k 10 240 python tools/latency.py > "$out/latency.jsonl" 2> "$out/latency.err" && \
+PV_LAT_CACHED=1 timeout -k 10 240 python tools/latency.py > "$out/latency_cached.jsonl" 2>> "$out/latency.err" && \
 step rocprof && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e \
     > "$out/prof.log" 2>&1 && \
