@@ -81,6 +81,12 @@ W_MAD_GROUPED = int(W_MUL_GROUPED * 100 + W_SQ_GROUPED * 55)
 W_MUL_KEYED, W_SQ_KEYED = 650.0, 175.5
 W_MUL_KEYPREP, W_SQ_KEYPREP = 1547.5, 1321.0
 W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
+# wide key format (radix-256 comb, --key-format wide; C3's node keys by default):
+# 24 doublings and 32 key adds per verify; 8 tables x 128 multiples per key
+# (host op counts, tests/test_hostcheck.py::test_keyed_wide_raw_vectors_and_op_counts)
+W_MUL_KEYED_WIDE, W_SQ_KEYED_WIDE = 414.0, 159.5
+W_MUL_KEYPREP_WIDE, W_SQ_KEYPREP_WIDE = 18219.5, 7656.0
+W_MAD_KEYED_WIDE = int(W_MUL_KEYED_WIDE * 100 + W_SQ_KEYED_WIDE * 55)
 # v_mad_u64_u32 issue ceiling of one MI355X measured by tools/ubench/mad_peak.hip
 # (profiles/r01_mad_peak.json, best over 1..8 waves/SIMD): lane-ops/s, whole chip.
 P_MAD_PER_S = 3.3896e13
@@ -719,6 +725,8 @@ def main():
                     help='signatures per GPU (default: the config\'s); spell it --count under torch.distributed.run')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true', help='skip the host-buffer (PCIe-inclusive) measurement')
+    ap.add_argument('--key-format', choices=('auto', 'narrow', 'wide'), default='auto',
+                    help='prepared-key format: auto = wide (radix-256 comb) for node keys (c3), narrow for key pools')
     ap.add_argument('--no-key-cache', action='store_true',
                     help='c3/c4: re-decompress every key per signature instead of preparing each distinct key once')
     ap.add_argument('--sequential', action='store_true',
@@ -767,7 +775,9 @@ def main():
         n -= n % n_nodes
     batch = SyntheticBatch(local, n, cfg['mlen'], cfg=cfg['cfg'], first=rank * n, key_mod=cfg['key_mod'],
                            mode=cfg['mode'], mlen_max=cfg['mlen_max'], n_nodes=n_nodes)
-    key_cache = batch.use_key_cache(not args.no_key_cache)   # keys repeat in c3 (node keys) and c4 (key pool)
+    # keys repeat in c3 (node keys: the wide comb) and c4 (key pool: the narrow one)
+    wide = args.key_format == 'wide' or (args.key_format == 'auto' and cfg['mode'] == synth.COMMIT)
+    key_cache = batch.use_key_cache(not args.no_key_cache, wide=wide)
     batch.make_slots()
     torch.cuda.synchronize()
     pipelined = not args.sequential
@@ -890,7 +900,11 @@ def main():
     kernel_ms_on = ('{} sequential calibration steps right before the timed region (pipelined launches overlap)'
                     .format(calib) if pipelined else 'the timed steps')
     curve_mode, deferred = nat.curve_stats(local)
-    if key_cache:
+    if key_cache and batch.wide:
+        kernel, work = 'k_curve<keyed, wide>', W_MAD_KEYED_WIDE * n
+        wpv = {'fe_mul': W_MUL_KEYED_WIDE, 'fe_sq': W_SQ_KEYED_WIDE, 'mad': W_MAD_KEYED_WIDE,
+               'per_distinct_key': {'fe_mul': W_MUL_KEYPREP_WIDE, 'fe_sq': W_SQ_KEYPREP_WIDE}}
+    elif key_cache:
         kernel, work = 'k_curve<keyed>', W_MAD_KEYED * n
         wpv = {'fe_mul': W_MUL_KEYED, 'fe_sq': W_SQ_KEYED, 'mad': W_MAD_KEYED,
                'per_distinct_key': {'fe_mul': W_MUL_KEYPREP, 'fe_sq': W_SQ_KEYPREP}}
@@ -924,8 +938,8 @@ def main():
                    'signatures_per_gpu': n, 'msg_bytes': [cfg['mlen'], cfg['mlen_max']] if cfg['mlen'] != cfg['mlen_max']
                    else cfg['mlen'], 'mean_msg_bytes': round(batch.blob_bytes / max(1, n), 1),
                    'key_pool': cfg['key_mod'] or ('node keys' if cfg['mode'] == synth.COMMIT else 'distinct'),
-                   'key_cache': 'prepared once per step per distinct key (inside the timed step)' if key_cache
-                   else 'off', 'tampered': int(tamper.sum()),
+                   'key_cache': 'prepared once per step per distinct key (inside the timed step), {} format'.format(
+                       'wide (radix-256 comb)' if batch.wide else 'narrow (radix-16 comb)') if key_cache else 'off', 'tampered': int(tamper.sum()),
                    'parallelism': 'dp{} (disjoint index shards) + {} all-gather of verdict bitmaps'.format(
                        world, 'RCCL' if backend == 'nccl' else backend + ' (rehearsal, ranks share GPU 0)')
                    if world > 1 else 'single GPU'},

@@ -162,6 +162,25 @@ int pv_keycache_add(const uint8_t *pk, uint64_t k);
 int pv_keycache_clear(void);
 int pv_keycache_size(uint64_t *count);
 
+/* Wide prepared keys (node keys): the same comb with radix-256 windows --
+ * affine multiples k * 2^(32 q) * (-A), k = 0..128, q = 0..7 (129 entries of
+ * 32 words per table) + status + padding, PV_KEY_WORDS_WIDE words (132 KB) per
+ * key.  A verify then needs 24 doublings and 32 key adds instead of 28 and 64;
+ * the preparation costs ~16x the default format's, so it pays for keys that
+ * sign many messages per preparation (a pool's node keys, C3).  Same verdicts.
+ * Preparation runs 8 lanes per key (one per table).  Async forms as
+ * pv_*_device_async (slot 0 or 1, enqueue only). */
+#define PV_KEY_WORDS_WIDE 33056u
+int pv_keys_prepare_wide_device(const uint8_t *pk, uint64_t k, uint32_t *ktab, int device, void *stream);
+int pv_keys_prepare_wide_device_async(const uint8_t *pk, uint64_t k, uint32_t *ktab, int device, void *stream,
+                                      int slot);
+int pv_verify_keyed_wide_device(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk, const uint8_t *sig,
+                                const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n, uint8_t *verdict,
+                                uint64_t *bitmap, int device, void *stream);
+int pv_verify_keyed_wide_device_async(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk,
+                                      const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n,
+                                      uint8_t *verdict, uint64_t *bitmap, int device, void *stream, int slot);
+
 /* SHA-256 / Merkle tree hashing.
  *   pv_sha256_batch[_device]  digests[i] (32 bytes) = SHA-256(prefix || M_i); prefix -1 = none,
  *                             0..255 = that single byte.  Replaces the per-request

@@ -27,6 +27,7 @@
 #include "pv_kernels.h"
 
 static_assert(PV_KEY_WORDS == (unsigned)pv::KEYTAB_WORDS, "prepared-key layout");
+static_assert(PV_KEY_WORDS_WIDE == (unsigned)pv::KEYTAB_WIDE_WORDS, "wide prepared-key layout");
 
 namespace {
 
@@ -671,14 +672,14 @@ bool lat_fused(const Device& d, const uint32_t* ktab, uint64_t n) {
   return !ktab && d.mode != CurveMode::Grouped && n <= d.lat_max && d.lat_quad;
 }
 // small keyed batches: one k_verify_quad_keyed launch
-bool lat_keyed(const Device& d, const uint32_t* ktab, uint64_t n) {
-  return ktab && n <= d.lat_keyed_max && d.lat_quad;
+bool lat_keyed(const Device& d, const uint32_t* ktab, uint64_t n, bool wide) {
+  return ktab && !wide && n <= d.lat_keyed_max && d.lat_quad;
 }
 
 int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                  const uint64_t* off, uint64_t n, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
-                 const uint32_t* kidx) {
-  if (lat_keyed(d, ktab, n)) return PV_OK;   // k_verify_quad_keyed runs the whole verify
+                 const uint32_t* kidx, bool wide) {
+  if (lat_keyed(d, ktab, n, wide)) return PV_OK;   // k_verify_quad_keyed runs the whole verify
   if (lat_fused(d, ktab, n)) {
     // k_verify_quad runs the whole verify; only the deferred counter is reset
     HIP_OK(w.qc.ensure(2));
@@ -707,9 +708,9 @@ int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig,
 
 int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                   const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
-                  const uint32_t* kidx) {
+                  const uint32_t* kidx, bool wide) {
   const bool half = !ktab && d.mode != CurveMode::Grouped;
-  if (lat_keyed(d, ktab, n)) {
+  if (lat_keyed(d, ktab, n, wide)) {
     // small keyed batch: one launch, the comb split over the signature's two
     // lane quads (the hashed key bytes are pk[kidx[i]])
     HIP_OK(pv::launch_verify_quad_keyed(pk, true, sig, blob, off, n, nullptr, ktab, kidx, d.bw.p, verdict, bm, s));
@@ -734,7 +735,8 @@ int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig
     d.last_ws = (int)(&w - d.ws);
   } else {
     HIP_OK(pv::launch_curve(pk, sig, w.h.p, w.pre.p, d.btab.p, w.scratch.p, w.scratch.cap / pv::ATAB_WORDS, verdict,
-                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p, w.qc.p + 1));
+                            bm, n, ktab ? d.curve_blocks_keyed : d.curve_blocks, s, ktab, kidx, d.bw.p, w.qc.p + 1,
+                            wide));
   }
   return PV_OK;
 }
@@ -742,7 +744,8 @@ int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig
 // enqueue hash + curve for device-resident inputs on stream s with workspace w
 int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                    const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed,
-                   float* ms_hash, float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr) {
+                   float* ms_hash, float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr,
+                   bool wide = false) {
   if (n == 0) return PV_OK;
   const bool live = !timed && d.live_timing;
   hipEvent_t* lev = nullptr;
@@ -764,12 +767,12 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
   if (rc) return rc;
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
   if (lev) HIP_OK(hipEventRecord(lev[0], s));
-  rc = enqueue_prep(d, w, pk, sig, blob, off, n, bm, s, ktab, kidx);
+  rc = enqueue_prep(d, w, pk, sig, blob, off, n, bm, s, ktab, kidx, wide);
   if (rc) return rc;
   // the "hash" interval also holds the scalar stage of the half-size path
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (lev) HIP_OK(hipEventRecord(lev[1], s));
-  rc = enqueue_curve(d, w, pk, sig, blob, off, n, verdict, bm, s, ktab, kidx);
+  rc = enqueue_curve(d, w, pk, sig, blob, off, n, verdict, bm, s, ktab, kidx, wide);
   if (rc) return rc;
   rc = ws_end(w, s);
   if (rc) return rc;
@@ -1485,6 +1488,81 @@ int pv_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const 
   if (rc) return rc;
   HIP_OK(hipStreamSynchronize(s));
   return PV_OK;
+}
+
+// wide key format (radix-256 comb): preparation on 8 lanes per key into
+// kscr / kscr2 (the slot's key scratch), verification through k_curve<true, 1>
+static int keys_prepare_wide(Device& d, const uint8_t* pk, uint64_t k, uint32_t* ktab, hipStream_t s, int slot) {
+  int rc = ws_begin(d.ws[slot], s);
+  if (rc) return rc;
+  DevBuf<uint32_t>& scr = slot ? d.kscr2 : d.kscr;
+  HIP_OK(scr.ensure((8 * k + 63) / 64 * 64 * (uint64_t)pv::KEYTAB_WIDE_SCRATCH));
+  HIP_OK(pv::launch_keys_wide(pk, k, ktab, scr.p, s));
+  return ws_end(d.ws[slot], s);
+}
+
+int pv_keys_prepare_wide_device(const uint8_t* pk, uint64_t k, uint32_t* ktab, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (k == 0) return PV_OK;
+  if (!pk || !ktab) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(d->ord));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  const int rc = keys_prepare_wide(*d, pk, k, ktab, s, 0);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_keys_prepare_wide_device_async(const uint8_t* pk, uint64_t k, uint32_t* ktab, int device, void* stream,
+                                      int slot) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
+  if (k == 0) return PV_OK;
+  if (!pk || !ktab) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(d->ord));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
+  return keys_prepare_wide(*d, pk, k, ktab, s, slot);
+}
+
+int pv_verify_keyed_wide_device(const uint32_t* ktab, const uint32_t* key_idx, const uint8_t* pk, const uint8_t* sig,
+                                const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n, uint8_t* verdict,
+                                uint64_t* bitmap, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n == 0) return PV_OK;
+  if (!ktab || !key_idx || !pk || !sig || !msg_blob || !msg_off || !verdict) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(d->ord));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  int rc = enqueue_verify(*d, d->ws[0], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr, ktab,
+                          key_idx, true);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s));
+  return PV_OK;
+}
+
+int pv_verify_keyed_wide_device_async(const uint32_t* ktab, const uint32_t* key_idx, const uint8_t* pk,
+                                      const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n,
+                                      uint8_t* verdict, uint64_t* bitmap, int device, void* stream, int slot) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
+  if (n == 0) return PV_OK;
+  if (!ktab || !key_idx || !pk || !sig || !msg_blob || !msg_off || !verdict || !bitmap)
+    return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(d->ord));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
+  return enqueue_verify(*d, d->ws[slot], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr,
+                        ktab, key_idx, true);
 }
 
 int pv_time_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const uint8_t* pk, const uint8_t* sig,

@@ -47,7 +47,8 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab = nullptr,
                         const uint32_t* kidx = nullptr, const uint32_t* bw = nullptr,
-                        unsigned long long* tasks = nullptr);   // wave task queue counter (zeroed here)
+                        unsigned long long* tasks = nullptr,    // wave task queue counter (zeroed here)
+                        bool wide = false);                     // ktab in the wide (radix-256) key format
 
 // Half-size scalar path (generic batches, pv_lattice.h):
 //   launch_lattice   pre-checks (-> pre) and h mod L -> (c, d, s') records
@@ -105,6 +106,12 @@ hipError_t launch_curve_half(const uint8_t* pk, const uint8_t* sig, const uint32
 constexpr int KEYTAB_WORDS = 8 * 9 * 32 + 32;
 constexpr int KEYTAB_SCRATCH = 64 * 40;   // projective entries + prefix products (lane-interleaved per 64 keys)
 hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
+// wide key format (radix-256 comb, node keys): KEYTAB_WIDE_WORDS words per key,
+// KEYTAB_WIDE_SCRATCH words of scratch per (key, table) lane (8 lanes per key,
+// lane-interleaved per 64)
+constexpr int KEYTAB_WIDE_WORDS = 8 * 129 * 32 + 32;
+constexpr int KEYTAB_WIDE_SCRATCH = 128 * 40;
+hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
 // latency mode for prepared keys (k_verify_quad_keyed): the whole verify of n
 // signatures in one launch, signature e's key = ktab entry kidx[i] with i =
 // list ? list[e] : e; the hashed key bytes are pk + 32 * (pk_by_key ? kidx[i] : i).

@@ -33,6 +33,8 @@ namespace pv {
 #define PV_CURVE_WAVES 2
 #endif
 
+static_assert(KEYTAB_WIDE_WORDS == KEYW_WORDS && KEYTAB_WIDE_SCRATCH == KEYW_SCRATCH && KEYTAB_WORDS == KEY_WORDS,
+              "prepared-key layouts");
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
                   AT_WORDS == ATAB_LAT_WORDS &&
                   KEY_WORDS == KEYTAB_WORDS && KEY_SCRATCH == KEYTAB_SCRATCH && BT_CHUNKS == BTAB_CHUNKS &&
@@ -318,7 +320,7 @@ hipError_t launch_btable_init(uint32_t* btab, hipStream_t s) {
 // points awaiting the shared inversion) and takes CURVE_K signatures per round:
 // gid, gid + nthreads, ... , gid + (K-1) nthreads.  Each wavefront covers 64
 // consecutive signatures per k, so each ballot is one aligned bitmap word.
-template <bool KEYED>
+template <bool KEYED, int KF>
 __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uint8_t* __restrict__ pk,
                                                                         const uint8_t* __restrict__ sig,
                                                                         const uint32_t* __restrict__ hin,
@@ -355,8 +357,8 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
     const uint64_t t = wave_task(tasks);
     if (t >= ntasks) break;
     const uint64_t i0 = t * PER + (uint64_t)ln;
-    const uint32_t okm = curve_group<KEYED, KEYED ? CURVE_BLOCK : 1>(pk, sig, hin, pre, i0, 64, n, lane, btab, ktab,
-                                                                      kidx, bw, dg + threadIdx.x);
+    const uint32_t okm = curve_group<KEYED, KEYED ? CURVE_BLOCK : 1, KF>(pk, sig, hin, pre, i0, 64, n, lane, btab,
+                                                                          ktab, kidx, bw, dg + threadIdx.x);
 #pragma unroll
     for (int k = 0; k < CURVE_K; ++k) {
       const uint64_t i = i0 + 64ull * (uint64_t)k;
@@ -372,17 +374,17 @@ __global__ __launch_bounds__(CURVE_BLOCK, PV_CURVE_WAVES) void k_curve(const uin
 
 hipError_t curve_occupancy(int* blocks_per_cu, bool keyed) {
   return keyed ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu,
-                                                              reinterpret_cast<const void*>(k_curve<true>),
+                                                              reinterpret_cast<const void*>(k_curve<true, 0>),
                                                               CURVE_BLOCK, 0)
                : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu,
-                                                              reinterpret_cast<const void*>(k_curve<false>),
+                                                              reinterpret_cast<const void*>(k_curve<false, 0>),
                                                               CURVE_BLOCK, 0);
 }
 
 hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre,
                         const uint32_t* btab, uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verdict,
                         uint64_t* bitmap, uint64_t n, int blocks, hipStream_t s, const uint32_t* ktab,
-                        const uint32_t* kidx, const uint32_t* bw, unsigned long long* tasks) {
+                        const uint32_t* kidx, const uint32_t* bw, unsigned long long* tasks, bool wide) {
   if (n == 0) return hipSuccess;
   // one wave task = 64 * CURVE_K signatures, CURVE_BLOCK / 64 waves per block
   const uint64_t ntasks = (n + 64ull * CURVE_K - 1) / (64ull * CURVE_K);
@@ -394,11 +396,14 @@ hipError_t launch_curve(const uint8_t* pk, const uint8_t* sig, const uint32_t* h
   if (!tasks) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(tasks, 0, sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
-  if (ktab)
-    hipLaunchKernelGGL(k_curve<true>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
+  if (ktab && wide)
+    hipLaunchKernelGGL((k_curve<true, 1>), dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
+                       verdict, bitmap, n, ktab, kidx, bw, tasks);
+  else if (ktab)
+    hipLaunchKernelGGL((k_curve<true, 0>), dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
                        verdict, bitmap, n, ktab, kidx, bw, tasks);
   else
-    hipLaunchKernelGGL(k_curve<false>, dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
+    hipLaunchKernelGGL((k_curve<false, 0>), dim3((uint32_t)b), dim3(CURVE_BLOCK), 0, s, pk, sig, h, pre, btab, scratch,
                        verdict, bitmap, n, nullptr, nullptr, nullptr, tasks);
   return hipGetLastError();
 }
@@ -846,6 +851,23 @@ __global__ __launch_bounds__(256, PV_KEYS_WAVES) void k_keys(const uint8_t* __re
 hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s) {
   if (k == 0) return hipSuccess;
   hipLaunchKernelGGL(k_keys, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, s, pk, k, ktab, scr);
+  return hipGetLastError();
+}
+
+// k_keys_wide: one lane per (key, table): lane g prepares table g % 8 of key
+// g / 8 (its 32 q doublings, 127 adds and one inversion); scratch
+// lane-interleaved per 64 lanes
+__global__ __launch_bounds__(64) void k_keys_wide(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
+                                                  uint32_t* __restrict__ scr) {
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (g < 8 * k)
+    key_prepare_wide_table<64>(ktab + (g >> 3) * (uint64_t)KEYW_WORDS,
+                               scr + (g / 64) * (uint64_t)(KEYW_SCRATCH * 64) + g % 64, pk + 32 * (g >> 3), (int)(g & 7));
+}
+
+hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_keys_wide, dim3((uint32_t)((8 * k + 63) / 64)), dim3(64), 0, s, pk, k, ktab, scr);
   return hipGetLastError();
 }
 

@@ -829,11 +829,193 @@ PV_HD void double_scalarmult_comb(ge_p2& out, const uint32_t hh[8], const uint32
   out = r2;
 }
 
-// R' = h(-A) + S B with -A's comb tables taken from a prepared key
+// ------------------------------------------------- wide comb (node keys)
+// The same 8-way comb with radix-256 windows: table q holds k * A_q for
+// k = 0..128 (129 affine entries, 132 KB per key), the signed digits are the
+// bytes of h + 0x80..80 minus 128, and a verify needs 3 x 8 = 24 doublings
+// and 32 key adds (+ the 16 base-point adds) instead of 28 and 64.  For keys
+// that sign many messages per preparation -- a pool's node keys (C3) -- where
+// the 16x larger preparation is amortised; the 9-entry format stays the
+// default for key pools (C4) and the latency kernels.
+constexpr int KW_ENT = 129;
+constexpr int KW_TABLE = KW_ENT * KT_ENTRY;          // 4128 words
+constexpr int KEYW_STATUS = COMB_Q * KW_TABLE;       // 33024
+constexpr int KEYW_WORDS = KEYW_STATUS + 32;         // 132224 B per key (128-byte multiple)
+// per (key, table) lane of k_keys_wide: projective multiples 1..128 and the
+// prefix products of their shared inversion (word w at scr[w * LS])
+constexpr int KWS_PREFIX = 128 * 30;
+constexpr int KEYW_SCRATCH = KWS_PREFIX + 128 * 10;
+
+// table q of a wide prepared key (kt = the key's KEYW_WORDS words); lane q = 0
+// also writes the status word (1 = A canonical, not small order, decodes)
+template <int LS = 1>
+PV_HD void key_prepare_wide_table(uint32_t* kt, uint32_t* scr, const uint8_t* pk, int q) {
+  uint32_t A[8];
+  load8(A, pk);
+  ge_p3 P;
+  const bool ok = y_is_canonical(A) && !has_small_order(A) && ge_frombytes_negate(P, A);
+  if (q == 0) kt[KEYW_STATUS] = ok ? 1u : 0u;
+  if (!ok) return;
+  if (q > 0) {   // A_q = 2^(32 q) (-A)
+    ge_p1p1 t;
+    ge_p2 r;
+    fe_copy(r.X, P.X);
+    fe_copy(r.Y, P.Y);
+    fe_copy(r.Z, P.Z);
+#pragma unroll 1
+    for (int d = 0; d + 1 < 32 * q; ++d) {
+      ge_p2_dbl(t, r);
+      ge_p1p1_to_p2(r, t);
+    }
+    ge_p2_dbl(t, r);
+    ge_p1p1_to_p3(P, t);
+  }
+  auto xyz = [&](int e) { return scr + 30 * e * LS; };
+  auto pre = [&](int e) { return scr + (KWS_PREFIX + 10 * e) * LS; };
+  ge_cached c1;
+  ge_p3_to_cached(c1, P);
+  ge_p3 Q = P;
+  store_fe<LS>(xyz(0), Q.X);
+  store_fe<LS>(xyz(0) + 10 * LS, Q.Y);
+  store_fe<LS>(xyz(0) + 20 * LS, Q.Z);
+  fe zacc;
+  fe_copy(zacc, Q.Z);
+  store_fe<LS>(pre(0), zacc);
+#pragma unroll 1
+  for (int e = 1; e < 128; ++e) {   // entry e = (e + 1) A_q
+    ge_p1p1 t;
+    ge_add_cached(t, Q, c1, false);
+    ge_p1p1_to_p3(Q, t);
+    store_fe<LS>(xyz(e), Q.X);
+    store_fe<LS>(xyz(e) + 10 * LS, Q.Y);
+    store_fe<LS>(xyz(e) + 20 * LS, Q.Z);
+    fe_mul(zacc, zacc, Q.Z);
+    store_fe<LS>(pre(e), zacc);
+  }
+  // one inversion for the 128 Z's, backward pass (key_prepare's)
+  uint32_t* tab = kt + q * KW_TABLE;
+  fe acc, u, z, x, y, d2;
+  fe_invert(acc, zacc);
+  fe_const_d2(d2);
+#pragma unroll 1
+  for (int e = 127; e >= 0; --e) {
+    load_fe<LS>(x, xyz(e));
+    load_fe<LS>(y, xyz(e) + 10 * LS);
+    fe zi;
+    if (e > 0) {
+      load_fe<LS>(u, pre(e - 1));
+      load_fe<LS>(z, xyz(e) + 20 * LS);
+      fe_mul(zi, acc, u);            // Z_e^-1
+      fe_mul(acc, acc, z);           // (Z_0 ... Z_{e-1})^-1
+    } else {
+      fe_copy(zi, acc);
+    }
+    fe_mul(x, x, zi);
+    fe_mul(y, y, zi);
+    fe ypx, ymx;
+    fe_add(ypx, y, x); fe_carry(ypx);
+    fe_sub(ymx, y, x); fe_carry(ymx);
+    fe_mul(u, x, y);
+    fe_mul(u, u, d2);
+    store_entry32(tab + (e + 1) * KT_ENTRY, ypx, ymx, u);
+  }
+  fe one, zero;
+  fe_1(one);
+  fe_0(zero);
+  store_entry32(tab, one, one, zero);   // k = 0: the identity
+}
+
+// R' = hh (-A) + ss B from a wide prepared key: windows w = 3..0 (bytes), 8
+// doublings apart; per window one affine add per table q with the signed
+// digit of byte w of word q, and on windows 2 and 0 the radix-2^16 base-point
+// digits of ss (high / low halves) as in double_scalarmult_comb.  Entries are
+// fetched one add ahead; the digit words live in dg (word k at dg[k * DS]).
 template <int DS = 1>
+PV_HD void double_scalarmult_comb_wide(ge_p2& out, const uint32_t hh[8], const uint32_t ss[8], const uint32_t* kt,
+                                       const uint32_t* bw, uint32_t* dg) {
+  {
+    uint32_t hp[8], sp[8];
+    sc_add_pattern(hp, hh, 0x80808080u);
+    sc_add_pattern(sp, ss, HALF_S_PATTERN);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      dg[k * DS] = hp[k];
+      dg[(8 + k) * DS] = sp[k];
+    }
+  }
+  ge_p3 acc;
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_p2 r2;
+  ge_nentry ea, eb;
+  int dA = (int)((dg[0] >> 24) & 255u) - 128;
+  load_nentry(ea, kt + (dA < 0 ? -dA : dA) * KT_ENTRY, dA < 0);
+#pragma unroll 1
+  for (int w = 3; w >= 0; --w) {
+    if (w != 3) {
+#pragma unroll 1
+      for (int k = 0; k < 7; ++k) {
+        ge_p2_dbl(t, r2);
+        ge_p1p1_to_p2(r2, t);
+      }
+      ge_p2_dbl(t, r2);
+      ge_p1p1_to_p3(acc, t);
+    }
+    const int sh8 = 8 * w;
+    const bool bwin = (w & 1) == 0;
+#pragma unroll 1
+    for (int q = 0; q < COMB_Q; q += 2) {
+      {
+        const int dn = (int)((dg[(q + 1) * DS] >> sh8) & 255u) - 128;
+        load_nentry(eb, kt + (q + 1) * KW_TABLE + (dn < 0 ? -dn : dn) * KT_ENTRY, dn < 0);
+        ge_madd_entry(t, acc, ea, dA < 0);
+        ge_p1p1_to_p3(acc, t);
+        dA = dn;
+      }
+      {
+        const bool last = q + 2 >= COMB_Q;
+        const bool more = !last || w > 0;
+        const int dn = (int)((dg[(last ? 0 : q + 2) * DS] >> ((last ? sh8 - 8 : sh8) & 31)) & 255u) - 128;
+        if (more) load_nentry(ea, kt + (last ? 0 : q + 2) * KW_TABLE + (dn < 0 ? -dn : dn) * KT_ENTRY, dn < 0);
+        ge_madd_entry(t, acc, eb, dA < 0);
+        if (!last || bwin) ge_p1p1_to_p3(acc, t);
+        else ge_p1p1_to_p2(r2, t);          // a doubling comes next: no T needed
+        dA = dn;
+      }
+    }
+    if (bwin) {
+      const int sh16 = 8 * w;   // w = 2: high half of each word, w = 0: low half
+      ge_nentry ba, bb;
+      int db = (int)((dg[8 * DS] >> sh16) & 0xffffu) - 32768;
+      load_nentry(ba, bw + (db < 0 ? -db : db) * BT_WORDS, db < 0);
+#pragma unroll 1
+      for (int q = 0; q < COMB_Q; q += 2) {
+        const int d1 = (int)((dg[(8 + q + 1) * DS] >> sh16) & 0xffffu) - 32768;
+        load_nentry(bb, bw + (q + 1) * BW_TABLE + (d1 < 0 ? -d1 : d1) * BT_WORDS, d1 < 0);
+        ge_madd_entry(t, acc, ba, db < 0);
+        ge_p1p1_to_p3(acc, t);
+        const bool last = q + 2 >= COMB_Q;
+        const int d2 = last ? 0 : (int)((dg[(8 + q + 2) * DS] >> sh16) & 0xffffu) - 32768;
+        if (!last) load_nentry(ba, bw + (q + 2) * BW_TABLE + (d2 < 0 ? -d2 : d2) * BT_WORDS, d2 < 0);
+        ge_madd_entry(t, acc, bb, d1 < 0);
+        if (!last) ge_p1p1_to_p3(acc, t);
+        else ge_p1p1_to_p2(r2, t);
+        db = d2;
+      }
+    }
+  }
+  out = r2;
+}
+
+// key formats of prepared keys: 0 = the 9-entry comb (KEY_WORDS), 1 = wide (KEYW_WORDS)
+template <int KF>
+PV_HD constexpr int key_words() { return KF ? KEYW_WORDS : KEY_WORDS; }
+
+// R' = h(-A) + S B with -A's comb tables taken from a prepared key
+template <int DS = 1, int KF = 0>
 PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, const uint32_t* dig_src,
                              const uint32_t* bw, uint32_t* dg) {
-  if (!kt[KEY_STATUS]) return false;
+  if (!kt[KF ? KEYW_STATUS : KEY_STATUS]) return false;
   uint32_t hh[8], S[8];
   {
     uint32_t dig[16];
@@ -842,7 +1024,8 @@ PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, 
     sc_reduce64(hh, dig);
   }
   load8(S, sig + 32);
-  double_scalarmult_comb<DS>(rp, hh, S, kt, bw, dg);
+  if constexpr (KF != 0) double_scalarmult_comb_wide<DS>(rp, hh, S, kt, bw, dg);
+  else double_scalarmult_comb<DS>(rp, hh, S, kt, bw, dg);
   return true;
 }
 
@@ -881,7 +1064,7 @@ PV_HD void batch_invert_z(uint32_t* pts, int K) {
 // shared inversion.  scratch = LANE_WORDS words owned by this lane.
 // KEYED: signature i uses prepared key kidx[i] (comb tables in ktab; btab
 // then holds the even chunk tables 0, 2, 4, 6 and bg all eight).
-template <bool KEYED, int DS = 1>
+template <bool KEYED, int DS = 1, int KF = 0>
 PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t* h, const uint8_t* pre, uint64_t i0,
                            uint64_t stride, uint64_t n, uint32_t* scratch, const uint32_t* btab,
                            const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr,
@@ -897,7 +1080,8 @@ PV_HD uint32_t curve_group(const uint8_t* pk, const uint8_t* sig, const uint32_t
     bool ok = false;
     if (i < n && pre[i]) {
       if constexpr (KEYED)
-        ok = curve_point_keyed<DS>(rp, ktab + (uint64_t)kidx[i] * KEY_WORDS, sig + 64 * i, h + 16 * i, bg, dg);
+        ok = curve_point_keyed<DS, KF>(rp, ktab + (uint64_t)kidx[i] * key_words<KF>(), sig + 64 * i, h + 16 * i, bg,
+                                       dg);
       else
         ok = curve_point(rp, pk + 32 * i, sig + 64 * i, h + 16 * i, scratch, btab);
     }

@@ -50,6 +50,13 @@ SIGNATURES = [
     ('pv_verify_keyed_device_async', ctypes.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int]),
     ('pv_keys_prepare_device_async', ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp, ctypes.c_int]),
+    ('pv_keys_prepare_wide_device', ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp]),
+    ('pv_keys_prepare_wide_device_async', ctypes.c_int,
+     [_vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp, ctypes.c_int]),
+    ('pv_verify_keyed_wide_device', ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_verify_keyed_wide_device_async', ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int]),
     ('pv_sha256_batch', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int32, _vp]),
     ('pv_sha256_batch_device', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int32, _vp, ctypes.c_int, _vp]),
     ('pv_merkle_root', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
@@ -302,6 +309,7 @@ def pack_messages(msgs):
 
 PV_FLAG_DEDUP_KEYS = 1
 PV_KEY_WORDS = 2336
+PV_KEY_WORDS_WIDE = 33056
 
 
 def verify_batch_arrays(pk, sig, blob, off, device_mask=0, dedup_keys=True):

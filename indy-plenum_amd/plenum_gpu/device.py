@@ -54,6 +54,7 @@ class SyntheticBatch:
                                             _p(self.sender), dev.index, _stream(dev)))
         self.keys = None   # (unique pk (k,32), key index (n,)) once use_key_cache() ran
         self.ktab = None
+        self.wide = False  # wide (radix-256) key format: node keys
 
     def key_index(self):
         """(unique keys, key index) of this batch from the synth spec: COMMIT
@@ -80,23 +81,28 @@ class SyntheticBatch:
             first = first[present]
         return self.pk[first].contiguous(), kidx.to(torch.int32).contiguous()
 
-    def use_key_cache(self, on=True):
-        """Verify through prepared keys (pv_keys_prepare_device + keyed kernels)."""
+    def use_key_cache(self, on=True, wide=False):
+        """Verify through prepared keys (pv_keys_prepare_device + keyed kernels);
+        wide: the radix-256 key format (pv_keys_prepare_wide_device), for keys
+        that sign many messages per preparation (node keys)."""
         if not on:
             self.keys = self.ktab = None
+            self.wide = False
             return False
         ki = self.key_index()
         if ki is None:
             return False
         self.keys = ki
-        self.ktab = torch.empty(ki[0].shape[0] * nat.PV_KEY_WORDS, dtype=torch.int32, device=self.device)
+        self.wide = bool(wide)
+        words = nat.PV_KEY_WORDS_WIDE if self.wide else nat.PV_KEY_WORDS
+        self.ktab = torch.empty(ki[0].shape[0] * words, dtype=torch.int32, device=self.device)
         return True
 
     def prepare_keys(self):
         upk, _ = self.keys
-        nat._check('pv_keys_prepare_device',
-                   nat.load().pv_keys_prepare_device(_p(upk), upk.shape[0], _p(self.ktab), self.device.index,
-                                                     _stream(self.device)))
+        fn = 'pv_keys_prepare_wide_device' if self.wide else 'pv_keys_prepare_device'
+        nat._check(fn, getattr(nat.load(), fn)(_p(upk), upk.shape[0], _p(self.ktab), self.device.index,
+                                               _stream(self.device)))
 
     def verify(self):
         """One pass of the hot path over the batch (hash + curve kernels; with
@@ -105,10 +111,10 @@ class SyntheticBatch:
         if self.keys is not None:
             self.prepare_keys()
             upk, kidx = self.keys
-            nat._check('pv_verify_keyed_device',
-                       lib.pv_verify_keyed_device(_p(self.ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob),
-                                                  _p(self.off), self.n, _p(self.verdict), _p(self.bitmap),
-                                                  self.device.index, _stream(self.device)))
+            fn = 'pv_verify_keyed_wide_device' if self.wide else 'pv_verify_keyed_device'
+            nat._check(fn, getattr(lib, fn)(_p(self.ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob),
+                                            _p(self.off), self.n, _p(self.verdict), _p(self.bitmap),
+                                            self.device.index, _stream(self.device)))
             return self.verdict
         nat._check('pv_verify_batch_device',
                    lib.pv_verify_batch_device(_p(self.pk), _p(self.sig), _p(self.blob), _p(self.off), self.n,
@@ -133,11 +139,11 @@ class SyntheticBatch:
         dev = self.device.index
         if self.keys is not None:
             upk, kidx = self.keys
-            nat._check('pv_keys_prepare_device_async',
-                       lib.pv_keys_prepare_device_async(_p(upk), upk.shape[0], _p(ktab), dev, s, slot))
-            nat._check('pv_verify_keyed_device_async',
-                       lib.pv_verify_keyed_device_async(_p(ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob),
-                                                        _p(self.off), self.n, _p(verdict), _p(bitmap), dev, s, slot))
+            w = '_wide' if self.wide else ''
+            fp, fv = 'pv_keys_prepare{}_device_async'.format(w), 'pv_verify_keyed{}_device_async'.format(w)
+            nat._check(fp, getattr(lib, fp)(_p(upk), upk.shape[0], _p(ktab), dev, s, slot))
+            nat._check(fv, getattr(lib, fv)(_p(ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob), _p(self.off),
+                                            self.n, _p(verdict), _p(bitmap), dev, s, slot))
         else:
             nat._check('pv_verify_batch_device_async',
                        lib.pv_verify_batch_device_async(_p(self.pk), _p(self.sig), _p(self.blob), _p(self.off),
@@ -149,6 +155,8 @@ class SyntheticBatch:
         lib = nat.load()
         a, b = ctypes.c_float(), ctypes.c_float()
         if self.keys is not None:
+            if self.wide:
+                raise NotImplementedError('kernel timing of the wide key format: use _native.kernel_timing')
             upk, kidx = self.keys
             nat._check('pv_time_verify_keyed_device',
                        lib.pv_time_verify_keyed_device(_p(self.ktab), _p(kidx), _p(upk), _p(self.sig), _p(self.blob),

@@ -102,3 +102,52 @@ def test_keyed_device_latency_kernel(nat, n):
         assert (bits == v).all(), lat
         res.append(v)
     assert (res[0] == res[1]).all()
+
+
+def test_wide_keys_c3_shape_and_adversarial(nat, adversarial):
+    """Wide (radix-256) prepared keys on the GPU: a C3-shaped batch (25 node
+    keys, 250k COMMIT votes) equals the synthetic spec and the narrow format,
+    and the adversarial fixture (every refused, small-order, non-canonical and
+    mixed-order key) gives libsodium's verdicts through
+    pv_keys_prepare_wide_device + pv_verify_keyed_wide_device."""
+    import torch
+    from plenum_gpu import synth
+    from plenum_gpu.device import SyntheticBatch, _p, _stream
+    b = SyntheticBatch(0, 250_000, 0, cfg=3, mode=synth.COMMIT, first=0)
+    want = ~b.tamper.cpu().numpy().astype(bool)
+    res = []
+    for wide in (True, False):
+        assert b.use_key_cache(True, wide=wide)
+        b.bitmap.fill_(-1)
+        v = b.verify().cpu().numpy().astype(bool)
+        bits = np.unpackbits(b.bitmap.cpu().numpy().view(np.uint8), bitorder='little')[:b.n].astype(bool)
+        assert (v == want).all(), wide
+        assert (bits == v).all(), wide
+        res.append(v)
+    assert (res[0] == res[1]).all()
+    # adversarial fixture, one signature per row, keys deduplicated
+    rows = [r for r in split_sm(adversarial) if len(r[2]) >= 64]
+    pk = np.stack([np.frombuffer(r[1], np.uint8) for r in rows])
+    upk, kidx = np.unique(pk, axis=0, return_inverse=True)
+    msgs = [r[2][64:] for r in rows]
+    off = np.zeros(len(rows) + 1, np.int64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    dev = torch.device('cuda', 0)
+    t_upk = torch.from_numpy(np.ascontiguousarray(upk)).to(dev)
+    t_kidx = torch.from_numpy(np.ascontiguousarray(kidx.reshape(-1).astype(np.int32))).to(dev)
+    t_sig = torch.from_numpy(np.stack([np.frombuffer(r[2][:64], np.uint8) for r in rows])).to(dev)
+    t_blob = torch.zeros(int(off[-1]) + 64, dtype=torch.uint8, device=dev)
+    if off[-1]:
+        t_blob[:int(off[-1])] = torch.from_numpy(np.frombuffer(b''.join(msgs), np.uint8).copy()).to(dev)
+    t_off = torch.from_numpy(off).to(dev)
+    ktab = torch.empty(len(upk) * nat.PV_KEY_WORDS_WIDE, dtype=torch.int32, device=dev)
+    verdict = torch.empty(len(rows), dtype=torch.uint8, device=dev)
+    lib = nat.load()
+    nat._check('pv_keys_prepare_wide_device',
+               lib.pv_keys_prepare_wide_device(_p(t_upk), len(upk), _p(ktab), 0, _stream(dev)))
+    nat._check('pv_verify_keyed_wide_device',
+               lib.pv_verify_keyed_wide_device(_p(ktab), _p(t_kidx), _p(t_upk), _p(t_sig), _p(t_blob), _p(t_off),
+                                               len(rows), _p(verdict), None, 0, _stream(dev)))
+    got = verdict.cpu().numpy().astype(bool)
+    wrong = [rows[k][0] for k in range(len(rows)) if got[k] != rows[k][3]]
+    assert not wrong, wrong

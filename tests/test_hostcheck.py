@@ -370,6 +370,60 @@ def test_keyed_path_adversarial_bit_exact(hc, adversarial):
     assert (v.astype(bool) == want).all()
 
 
+def _run_keyed_wide(hc, pk, sig, blob, off):
+    upk, kidx = np.unique(pk, axis=0, return_inverse=True)
+    kidx = np.ascontiguousarray(kidx.reshape(-1), np.uint32)
+    upk = np.ascontiguousarray(upk, np.uint8)
+    n = len(pk)
+    v = np.zeros(n, np.uint8)
+    b = orc.padded(blob)
+    hc.hc_reset_counts()
+    hc.hc_verify_keyed_wide(_p(upk), ctypes.c_uint64(len(upk)), _p(kidx), _p(np.ascontiguousarray(sig)), _p(b),
+                            _p(np.ascontiguousarray(off)), ctypes.c_uint64(n), _p(v))
+    c, bad = counts(hc)
+    assert bad == 0
+    return v, c, len(upk)
+
+
+def test_keyed_wide_adversarial_bit_exact(hc, adversarial):
+    """Wide (radix-256) prepared keys: every adversarial key and signature gives
+    the fixture's verdict through key_prepare_wide_table + the wide comb, every
+    multiply bound-checked."""
+    pk, sig, blob, off, want = _adv_arrays(adversarial)
+    v, _, _ = _run_keyed_wide(hc, pk, sig, blob, off)
+    assert (v.astype(bool) == want).all()
+
+
+def test_keyed_wide_raw_vectors_and_op_counts(hc, raw_vectors):
+    """Raw vectors through the wide keyed path, and its work per verify / per
+    prepared key pinned for the bench (bench.W_*_KEYED_WIDE, W_*_KEYPREP_WIDE)."""
+    import bench
+    r = raw_vectors
+    pk, sig = r['pk'][:300], r['sig'][:300]
+    off = r['off'][:301] - r['off'][0]
+    blob = r['blob'][int(r['off'][0]):int(r['off'][300])]
+    v, _, _ = _run_keyed_wide(hc, pk, sig, blob, off)
+    assert (v == r['verdict'][:300]).all()
+    # one key signing 16 messages vs 16 keys: preparation and per-verify work
+    n = 16
+    seeds = np.frombuffer(os.urandom(32 * n), np.uint8).reshape(n, 32)
+    blob = np.frombuffer(os.urandom(256 * n), np.uint8)
+    off = np.arange(n + 1, dtype=np.uint64) * 256
+    spk, ssig = orc.sign_batch(seeds, blob, off)
+    hc.hc_btable((ctypes.c_uint32 * (8 * 129 * 32))())
+    _, c_many, k_many = _run_keyed_wide(hc, spk, ssig, blob, off)
+    one_pk = np.repeat(spk[:1], n, 0)
+    one_sig = np.repeat(ssig[:1], n, 0)
+    vb, c_one, k_one = _run_keyed_wide(hc, one_pk, one_sig, np.tile(blob[:256], n), off)
+    assert vb.all() and k_many == n and k_one == 1
+    prep_sq = (int(c_many[1]) - int(c_one[1])) / (n - 1)
+    assert prep_sq == bench.W_SQ_KEYPREP_WIDE
+    assert (int(c_one[1]) - prep_sq) / n == bench.W_SQ_KEYED_WIDE
+    prep_mul = (int(c_many[0]) - int(c_one[0])) / (n - 1)
+    assert abs(prep_mul - bench.W_MUL_KEYPREP_WIDE) <= 8.0, prep_mul
+    assert abs((int(c_one[0]) - prep_mul) / n - bench.W_MUL_KEYED_WIDE) <= 0.6, (int(c_one[0]) - prep_mul) / n
+
+
 def _run_keyed_quad(hc, pk, sig, blob, off):
     upk, kidx = np.unique(pk, axis=0, return_inverse=True)
     kidx = np.ascontiguousarray(kidx.reshape(-1), np.uint32)

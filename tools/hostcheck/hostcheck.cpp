@@ -253,6 +253,30 @@ void hc_verify_keyed(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const 
   free(pre);
 }
 
+// wide (radix-256) prepared keys: every table of every key on the host, then
+// the keyed curve stage with the wide comb (k_curve<true, 1>'s algorithm)
+void hc_verify_keyed_wide(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig, const uint8_t* blob,
+                          const uint64_t* off, uint64_t n, uint8_t* verdict) {
+  ensure_btab();
+  static uint32_t lane[LANE_WORDS];
+  uint32_t* ktab = (uint32_t*)calloc(k ? k * KEYW_WORDS : KEYW_WORDS, sizeof(uint32_t));
+  uint32_t* scr = (uint32_t*)calloc(KEYW_SCRATCH, sizeof(uint32_t));
+  for (uint64_t j = 0; j < k; ++j)
+    for (int q = 0; q < COMB_Q; ++q) key_prepare_wide_table(ktab + j * KEYW_WORDS, scr, pk + 32 * j, q);
+  free(scr);
+  uint32_t* h = (uint32_t*)calloc(n ? n * 16 : 16, sizeof(uint32_t));
+  uint8_t* pre = (uint8_t*)calloc(n ? n : 1, 1);
+  for (uint64_t i = 0; i < n; ++i)
+    pre[i] = hash_one(h + 16 * i, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+  for (uint64_t i0 = 0; i0 < n; i0 += CURVE_K) {
+    const uint32_t okm = curve_group<true, 1, 1>(pk, sig, h, pre, i0, 1, n, lane, g_btab_even, ktab, kidx, g_bw);
+    for (int q = 0; q < CURVE_K && i0 + q < n; ++q) verdict[i0 + q] = (okm >> q) & 1u;
+  }
+  free(ktab);
+  free(h);
+  free(pre);
+}
+
 // keyed latency kernel (k_verify_quad_keyed): prepared keys, each side's
 // comb share on an emulated quad, -R added on side 1, identity test
 void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
