@@ -31,7 +31,7 @@ import torch.distributed as dist  # noqa: E402
 
 from plenum_gpu import _native as nat  # noqa: E402
 from plenum_gpu import synth  # noqa: E402
-from plenum_gpu.device import SyntheticBatch, tally_device  # noqa: E402
+from plenum_gpu.device import SyntheticBatch, tally_device, tally_device_async  # noqa: E402
 from plenum_gpu.quorums import Quorums  # noqa: E402
 
 METRIC = 'Ed25519 verifies/sec at 1/2/4/8 MI355X vs libsodium on host cores'
@@ -796,12 +796,15 @@ def main():
         tally = dict(nb=nb, q=q, boff=torch.arange(nb + 1, dtype=torch.int64, device=dev) * n_nodes,
                      votes=[torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(slots)],
                      reached=[torch.empty(nb, dtype=torch.uint8, device=dev) for _ in range(slots)],
-                     gathered=[torch.empty(world * nb, dtype=torch.uint8, device=dev) for _ in range(slots)])
+                     gathered=[torch.empty(world * nb, dtype=torch.uint8, device=dev) for _ in range(slots)],
+                     bad=torch.zeros(1, dtype=torch.int32, device=dev))
 
     def finish(slot, verdict, bitmap):
         if tally is not None:
-            tally_device(verdict, batch.sender, tally['boff'], n_nodes, tally['q'], tally['votes'][slot],
-                         tally['reached'][slot])
+            # enqueue-only tally: the sender range flag is read once after the
+            # timed region, so no step waits on the host (steps stay pipelined)
+            tally_device_async(verdict, batch.sender, tally['boff'], n_nodes, tally['q'], tally['votes'][slot],
+                               tally['reached'][slot], tally['bad'], streams[slot] if pipelined else None)
         if world > 1:
             all_gather(gathered[slot], bitmap)
             if tally is not None:   # C3: batch-sharded tallies, gather the quorum bits
@@ -859,6 +862,8 @@ def main():
     tamper = batch.tamper.cpu().numpy().astype(bool)
     mism = 0
     used = min(slots, args.steps + args.warmup)
+    if tally is not None:
+        mism += int(tally['bad'].item() != 0)   # a sender index out of range in any step
     for slot in range(used):
         v_t, b_t, _ = batch.slot_out[slot]
         verdict = v_t.cpu().numpy().astype(bool)

@@ -229,6 +229,12 @@ int pv_tally_votes(const uint8_t *verdict, const uint32_t *sender, const uint64_
 int pv_tally_votes_device(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off,
                           uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t *votes, uint8_t *reached,
                           int device, void *stream);
+/* Enqueue-only form for pipelined callers: the kernel ORs 1 into the DEVICE
+ * word *bad when a sender index is >= n_nodes (the caller zeroes it and checks
+ * it once its stream is synchronised -- such a vote is never counted). */
+int pv_tally_votes_device_async(const uint8_t *verdict, const uint32_t *sender, const uint64_t *batch_off,
+                                uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t *votes,
+                                uint8_t *reached, uint32_t *bad, int device, void *stream);
 
 /* Batch keygen + sign (HOST memory): pk_out[i], sig_out[i] for seed i over
  * message i.  Deterministic (RFC 8032 / crypto_sign_detached). */

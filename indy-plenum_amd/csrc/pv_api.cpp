@@ -1732,6 +1732,23 @@ int pv_tally_votes_device(const uint8_t* verdict, const uint32_t* sender, const 
   return PV_OK;
 }
 
+int pv_tally_votes_device_async(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off,
+                                uint64_t n_batches, uint32_t n_nodes, uint32_t quorum, uint32_t* votes,
+                                uint8_t* reached, uint32_t* bad, int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (n_nodes == 0 || n_nodes > 1024) return fail(PV_EINVAL, "n_nodes must be in 1..1024");
+  if (!bad) return fail(PV_EINVAL, "null device buffer");
+  if (n_batches == 0) return PV_OK;
+  if (!verdict || !sender || !batch_off || !votes || !reached) return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(d->ord));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
+  HIP_OK(pv::launch_tally(verdict, sender, batch_off, n_batches, n_nodes, quorum, votes, reached, bad, s));
+  return PV_OK;
+}
+
 int pv_tally_votes(const uint8_t* verdict, const uint32_t* sender, const uint64_t* batch_off, uint64_t n_batches,
                    uint32_t n_nodes, uint32_t quorum, uint32_t* votes, uint8_t* reached) {
   std::lock_guard<std::mutex> lk(g_mu);

@@ -33,6 +33,8 @@ SIGNATURES = [
     ('pv_tally_votes', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     ('pv_tally_votes_device', ctypes.c_int,
      [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_int, _vp]),
+    ('pv_tally_votes_device_async', ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int, _vp]),
     ('pv_sign_batch', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     ('pv_sign_batch_device', ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
     ('pv_synth_device', ctypes.c_int,

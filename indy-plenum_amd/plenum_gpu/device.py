@@ -182,6 +182,20 @@ def verify_device(pk, sig, blob, off, verdict, bitmap=None):
     return verdict
 
 
+def tally_device_async(verdict, sender, batch_off, n_nodes, quorum, votes, reached, bad, stream=None):
+    """Enqueue the quorum tally on `stream` (default: the current stream) without
+    waiting; `bad` (int32 device tensor, zeroed by the caller) becomes nonzero if
+    a sender index is out of range (pv_tally_votes_device_async)."""
+    dev = verdict.device
+    nat.ensure_init(1 << dev.index)
+    nb = batch_off.shape[0] - 1
+    s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream(dev)
+    nat._check('pv_tally_votes_device_async',
+               nat.load().pv_tally_votes_device_async(_p(verdict), _p(sender), _p(batch_off), nb, n_nodes, quorum,
+                                                      _p(votes), _p(reached), _p(bad), dev.index, s))
+    return votes, reached
+
+
 def tally_device(verdict, sender, batch_off, n_nodes, quorum, votes, reached):
     dev = verdict.device
     nat.ensure_init(1 << dev.index)

@@ -142,3 +142,37 @@ def test_tally_device_rejects_out_of_range_sender():
     s[1] = 24
     tally_device(v, s, off, 25, 2, votes, reached)
     assert int(votes[0]) == 2 and int(reached[0]) == 1
+
+
+def test_tally_device_async_flag_and_side_stream():
+    """pv_tally_votes_device_async: enqueue-only on a side stream, same tallies
+    as the synchronous form; an out-of-range sender raises the device flag
+    (and is not counted) instead of failing the call."""
+    import torch
+    from plenum_gpu.device import tally_device, tally_device_async
+    dev = torch.device('cuda:0')
+    g = torch.Generator().manual_seed(7)
+    nb, nn = 1000, 25
+    v = (torch.rand(nb * nn, generator=g) > 0.2).to(torch.uint8).to(dev)
+    s = torch.randint(0, nn, (nb * nn,), generator=g, dtype=torch.int32).to(dev)
+    off = (torch.arange(nb + 1, dtype=torch.int64) * nn).to(dev)
+    want_v = torch.empty(nb, dtype=torch.int32, device=dev)
+    want_r = torch.empty(nb, dtype=torch.uint8, device=dev)
+    tally_device(v, s, off, nn, 17, want_v, want_r)
+    votes = torch.empty(nb, dtype=torch.int32, device=dev)
+    reached = torch.empty(nb, dtype=torch.uint8, device=dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = torch.cuda.Stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    tally_device_async(v, s, off, nn, 17, votes, reached, bad, st)
+    st.synchronize()
+    assert int(bad[0]) == 0
+    assert torch.equal(votes, want_v) and torch.equal(reached, want_r)
+    s[3] = nn
+    tally_device_async(v, s, off, nn, 17, votes, reached, bad)
+    torch.cuda.synchronize()
+    assert int(bad[0]) != 0
+    # the out-of-range vote is dropped: batch 0 counts the distinct valid senders left
+    vh, sh = v[:nn].cpu().tolist(), s[:nn].cpu().tolist()
+    assert int(votes[0]) == len({sh[m] for m in range(nn) if vh[m] and sh[m] < nn})
+    assert torch.equal(votes[1:], want_v[1:])
