@@ -82,10 +82,12 @@ W_MUL_KEYED, W_SQ_KEYED = 650.0, 175.5
 W_MUL_KEYPREP, W_SQ_KEYPREP = 1547.5, 1321.0
 W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
 # wide key format (radix-256 comb, --key-format wide; C3's node keys by default):
-# 24 doublings and 32 key adds per verify; 8 tables x 128 multiples per key
+# 24 doublings and 32 key adds per verify; 8 tables x 128 multiples per key,
+# built by 128 lanes that each redo the decode and A_q's doublings (latency over
+# work: 7.3x the one-lane-per-table work per key, 1.2 -> ~0.7 ms for 25 keys)
 # (host op counts, tests/test_hostcheck.py::test_keyed_wide_raw_vectors_and_op_counts)
 W_MUL_KEYED_WIDE, W_SQ_KEYED_WIDE = 414.0, 159.5
-W_MUL_KEYPREP_WIDE, W_SQ_KEYPREP_WIDE = 18219.5, 7656.0
+W_MUL_KEYPREP_WIDE, W_SQ_KEYPREP_WIDE = 69940.0, 126080.0
 W_MAD_KEYED_WIDE = int(W_MUL_KEYED_WIDE * 100 + W_SQ_KEYED_WIDE * 55)
 # v_mad_u64_u32 issue ceiling of one MI355X measured by tools/ubench/mad_peak.hip
 # (profiles/r01_mad_peak.json, best over 1..8 waves/SIMD): lane-ops/s, whole chip.

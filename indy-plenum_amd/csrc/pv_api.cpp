@@ -1496,7 +1496,7 @@ static int keys_prepare_wide(Device& d, const uint8_t* pk, uint64_t k, uint32_t*
   int rc = ws_begin(d.ws[slot], s);
   if (rc) return rc;
   DevBuf<uint32_t>& scr = slot ? d.kscr2 : d.kscr;
-  HIP_OK(scr.ensure((8 * k + 63) / 64 * 64 * (uint64_t)pv::KEYTAB_WIDE_SCRATCH));
+  HIP_OK(scr.ensure(k * pv::KEYTAB_WIDE_LANES * (uint64_t)pv::KEYTAB_WIDE_SCRATCH));
   HIP_OK(pv::launch_keys_wide(pk, k, ktab, scr.p, s));
   return ws_end(d.ws[slot], s);
 }

@@ -107,10 +107,11 @@ constexpr int KEYTAB_WORDS = 8 * 9 * 32 + 32;
 constexpr int KEYTAB_SCRATCH = 64 * 40;   // projective entries + prefix products (lane-interleaved per 64 keys)
 hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
 // wide key format (radix-256 comb, node keys): KEYTAB_WIDE_WORDS words per key,
-// KEYTAB_WIDE_SCRATCH words of scratch per (key, table) lane (8 lanes per key,
-// lane-interleaved per 64)
+// KEYTAB_WIDE_SCRATCH words of scratch per lane (KEYTAB_WIDE_LANES lanes per
+// key: 16 per table, lane-interleaved per 64)
 constexpr int KEYTAB_WIDE_WORDS = 8 * 129 * 32 + 32;
-constexpr int KEYTAB_WIDE_SCRATCH = 128 * 40;
+constexpr int KEYTAB_WIDE_LANES = 128;
+constexpr int KEYTAB_WIDE_SCRATCH = 8 * 40;
 hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s);
 // latency mode for prepared keys (k_verify_quad_keyed): the whole verify of n
 // signatures in one launch, signature e's key = ktab entry kidx[i] with i =

@@ -33,7 +33,8 @@ namespace pv {
 #define PV_CURVE_WAVES 2
 #endif
 
-static_assert(KEYTAB_WIDE_WORDS == KEYW_WORDS && KEYTAB_WIDE_SCRATCH == KEYW_SCRATCH && KEYTAB_WORDS == KEY_WORDS,
+static_assert(KEYTAB_WIDE_WORDS == KEYW_WORDS && KEYTAB_WIDE_SCRATCH == KEYW_SCRATCH && KEYTAB_WORDS == KEY_WORDS &&
+                  KEYTAB_WIDE_LANES == COMB_Q * KW_SLICES && KEYTAB_WIDE_LANES % 64 == 0,
               "prepared-key layouts");
 static_assert(BT_ENTRIES == BTAB_ENTRIES && BT_WORDS == BTAB_WORDS && LANE_WORDS == ATAB_WORDS &&
                   AT_WORDS == ATAB_LAT_WORDS &&
@@ -854,20 +855,21 @@ hipError_t launch_keys(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* 
   return hipGetLastError();
 }
 
-// k_keys_wide: one lane per (key, table): lane g prepares table g % 8 of key
-// g / 8 (its 32 q doublings, 127 adds and one inversion); scratch
-// lane-interleaved per 64 lanes
+// k_keys_wide: 128 lanes per key, lane g builds slice g % 16 of table
+// (g / 16) % 8 of key g / 128 (key_prepare_wide_slice: the doublings of A_q,
+// 8 multiples, one inversion); scratch lane-interleaved per 64 lanes
 __global__ __launch_bounds__(64) void k_keys_wide(const uint8_t* __restrict__ pk, uint64_t k, uint32_t* __restrict__ ktab,
                                                   uint32_t* __restrict__ scr) {
   const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-  if (g < 8 * k)
-    key_prepare_wide_table<64>(ktab + (g >> 3) * (uint64_t)KEYW_WORDS,
-                               scr + (g / 64) * (uint64_t)(KEYW_SCRATCH * 64) + g % 64, pk + 32 * (g >> 3), (int)(g & 7));
+  const uint64_t key = g / (COMB_Q * KW_SLICES);
+  if (key < k)
+    key_prepare_wide_slice<64>(ktab + key * (uint64_t)KEYW_WORDS, scr + (g / 64) * (uint64_t)(KEYW_SCRATCH * 64) + g % 64,
+                               pk + 32 * key, (int)((g / KW_SLICES) % COMB_Q), (int)(g % KW_SLICES));
 }
 
 hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint32_t* scr, hipStream_t s) {
   if (k == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_keys_wide, dim3((uint32_t)((8 * k + 63) / 64)), dim3(64), 0, s, pk, k, ktab, scr);
+  hipLaunchKernelGGL(k_keys_wide, dim3((uint32_t)(KEYTAB_WIDE_LANES * k / 64)), dim3(64), 0, s, pk, k, ktab, scr);
   return hipGetLastError();
 }
 

@@ -841,23 +841,37 @@ constexpr int KW_ENT = 129;
 constexpr int KW_TABLE = KW_ENT * KT_ENTRY;          // 4128 words
 constexpr int KEYW_STATUS = COMB_Q * KW_TABLE;       // 33024
 constexpr int KEYW_WORDS = KEYW_STATUS + 32;         // 132224 B per key (128-byte multiple)
-// per (key, table) lane of k_keys_wide: projective multiples 1..128 and the
-// prefix products of their shared inversion (word w at scr[w * LS])
-constexpr int KWS_PREFIX = 128 * 30;
-constexpr int KEYW_SCRATCH = KWS_PREFIX + 128 * 10;
+// k_keys_wide spreads a table over KW_SLICES lanes: lane (q, s) builds the
+// multiples k = KW_SLICE s + 1 .. KW_SLICE (s + 1) of A_q (its projective
+// points and the prefix products of their shared inversion in scratch, word w
+// at scr[w * LS]).  Every lane of a table redoes the 32 q doublings of A_q:
+// the chain (224 doublings for q = 7) bounds the kernel's latency either way,
+// and redoing it costs no barrier and no exchange between lanes.
+constexpr int KW_SLICES = 16;
+constexpr int KW_SLICE = 128 / KW_SLICES;            // 8 multiples per lane
+constexpr int KWS_PREFIX = KW_SLICE * 30;
+constexpr int KEYW_SCRATCH = KWS_PREFIX + KW_SLICE * 10;
 
-// table q of a wide prepared key (kt = the key's KEYW_WORDS words); lane q = 0
-// also writes the status word (1 = A canonical, not small order, decodes)
+PV_HD void ge_p3_cmov(ge_p3& h, const ge_p3& f, const ge_p3& g, bool c) {
+  fe_cmov(h.X, f.X, g.X, c);
+  fe_cmov(h.Y, f.Y, g.Y, c);
+  fe_cmov(h.Z, f.Z, g.Z, c);
+  fe_cmov(h.T, f.T, g.T, c);
+}
+
+// slice s of table q of a wide prepared key (kt = the key's KEYW_WORDS words);
+// lane (0, 0) also writes the status word (1 = A canonical, not small order,
+// decodes) and lane (q, 0) the identity entry k = 0 of table q
 template <int LS = 1>
-PV_HD void key_prepare_wide_table(uint32_t* kt, uint32_t* scr, const uint8_t* pk, int q) {
+PV_HD void key_prepare_wide_slice(uint32_t* kt, uint32_t* scr, const uint8_t* pk, int q, int s) {
   uint32_t A[8];
   load8(A, pk);
   ge_p3 P;
   const bool ok = y_is_canonical(A) && !has_small_order(A) && ge_frombytes_negate(P, A);
-  if (q == 0) kt[KEYW_STATUS] = ok ? 1u : 0u;
+  if (q == 0 && s == 0) kt[KEYW_STATUS] = ok ? 1u : 0u;
   if (!ok) return;
+  ge_p1p1 t;
   if (q > 0) {   // A_q = 2^(32 q) (-A)
-    ge_p1p1 t;
     ge_p2 r;
     fe_copy(r.X, P.X);
     fe_copy(r.Y, P.Y);
@@ -870,11 +884,32 @@ PV_HD void key_prepare_wide_table(uint32_t* kt, uint32_t* scr, const uint8_t* pk
     ge_p2_dbl(t, r);
     ge_p1p1_to_p3(P, t);
   }
-  auto xyz = [&](int e) { return scr + 30 * e * LS; };
-  auto pre = [&](int e) { return scr + (KWS_PREFIX + 10 * e) * LS; };
   ge_cached c1;
   ge_p3_to_cached(c1, P);
-  ge_p3 Q = P;
+  // Q = (KW_SLICE s + 1) A_q = s (8 A_q) + A_q: 4-bit ladder over s, MSB first
+  // (the extended-coordinate formulas are complete: the identity and equal
+  // operands need no special case)
+  ge_p3 P8 = P, Q, T;
+#pragma unroll 1
+  for (int d = 0; d < 3; ++d) {
+    ge_p3_dbl(t, P8);
+    ge_p1p1_to_p3(P8, t);
+  }
+  ge_cached c8;
+  ge_p3_to_cached(c8, P8);
+  ge_p3_0(Q);
+#pragma unroll 1
+  for (int b = 3; b >= 0; --b) {
+    ge_p3_dbl(t, Q);
+    ge_p1p1_to_p3(Q, t);
+    ge_add_cached(t, Q, c8, false);
+    ge_p1p1_to_p3(T, t);
+    ge_p3_cmov(Q, Q, T, (s >> b) & 1);
+  }
+  ge_add_cached(t, Q, c1, false);
+  ge_p1p1_to_p3(Q, t);
+  auto xyz = [&](int e) { return scr + 30 * e * LS; };
+  auto pre = [&](int e) { return scr + (KWS_PREFIX + 10 * e) * LS; };
   store_fe<LS>(xyz(0), Q.X);
   store_fe<LS>(xyz(0) + 10 * LS, Q.Y);
   store_fe<LS>(xyz(0) + 20 * LS, Q.Z);
@@ -882,8 +917,7 @@ PV_HD void key_prepare_wide_table(uint32_t* kt, uint32_t* scr, const uint8_t* pk
   fe_copy(zacc, Q.Z);
   store_fe<LS>(pre(0), zacc);
 #pragma unroll 1
-  for (int e = 1; e < 128; ++e) {   // entry e = (e + 1) A_q
-    ge_p1p1 t;
+  for (int e = 1; e < KW_SLICE; ++e) {   // entry e = (KW_SLICE s + e + 1) A_q
     ge_add_cached(t, Q, c1, false);
     ge_p1p1_to_p3(Q, t);
     store_fe<LS>(xyz(e), Q.X);
@@ -892,13 +926,13 @@ PV_HD void key_prepare_wide_table(uint32_t* kt, uint32_t* scr, const uint8_t* pk
     fe_mul(zacc, zacc, Q.Z);
     store_fe<LS>(pre(e), zacc);
   }
-  // one inversion for the 128 Z's, backward pass (key_prepare's)
-  uint32_t* tab = kt + q * KW_TABLE;
+  // one inversion for the slice's Z's, backward pass (key_prepare's)
+  uint32_t* tab = kt + q * KW_TABLE + (KW_SLICE * s + 1) * KT_ENTRY;
   fe acc, u, z, x, y, d2;
   fe_invert(acc, zacc);
   fe_const_d2(d2);
 #pragma unroll 1
-  for (int e = 127; e >= 0; --e) {
+  for (int e = KW_SLICE - 1; e >= 0; --e) {
     load_fe<LS>(x, xyz(e));
     load_fe<LS>(y, xyz(e) + 10 * LS);
     fe zi;
@@ -917,12 +951,14 @@ PV_HD void key_prepare_wide_table(uint32_t* kt, uint32_t* scr, const uint8_t* pk
     fe_sub(ymx, y, x); fe_carry(ymx);
     fe_mul(u, x, y);
     fe_mul(u, u, d2);
-    store_entry32(tab + (e + 1) * KT_ENTRY, ypx, ymx, u);
+    store_entry32(tab + e * KT_ENTRY, ypx, ymx, u);
   }
-  fe one, zero;
-  fe_1(one);
-  fe_0(zero);
-  store_entry32(tab, one, one, zero);   // k = 0: the identity
+  if (s == 0) {
+    fe one, zero;
+    fe_1(one);
+    fe_0(zero);
+    store_entry32(kt + q * KW_TABLE, one, one, zero);   // k = 0: the identity
+  }
 }
 
 // R' = hh (-A) + ss B from a wide prepared key: windows w = 3..0 (bytes), 8

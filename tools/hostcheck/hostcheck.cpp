@@ -262,7 +262,8 @@ void hc_verify_keyed_wide(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
   uint32_t* ktab = (uint32_t*)calloc(k ? k * KEYW_WORDS : KEYW_WORDS, sizeof(uint32_t));
   uint32_t* scr = (uint32_t*)calloc(KEYW_SCRATCH, sizeof(uint32_t));
   for (uint64_t j = 0; j < k; ++j)
-    for (int q = 0; q < COMB_Q; ++q) key_prepare_wide_table(ktab + j * KEYW_WORDS, scr, pk + 32 * j, q);
+    for (int q = 0; q < COMB_Q; ++q)
+      for (int sl = 0; sl < KW_SLICES; ++sl) key_prepare_wide_slice(ktab + j * KEYW_WORDS, scr, pk + 32 * j, q, sl);
   free(scr);
   uint32_t* h = (uint32_t*)calloc(n ? n * 16 : 16, sizeof(uint32_t));
   uint8_t* pre = (uint8_t*)calloc(n ? n : 1, 1);
