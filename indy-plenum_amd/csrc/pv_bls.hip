@@ -35,6 +35,9 @@ using namespace bn;
 constexpr int KEY_LINE_WORDS = N_LINES * LINE_WORDS;   // 2800 words per G2 point
 constexpr int MSG_WORDS = 4 * NL;                        // x_H, y_H, xq(-H), yq(-H)
 constexpr int BLS_BLOCK = 256;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PV_BN_MILLER_REGS)
+static_assert(BLS_BLOCK == bn::MF_LANES, "the Miller loop's LDS accumulator is laid out per check block");
+#endif
 // waves per SIMD the check kernel is compiled for: 1 (512 registers) measured
 // 1.77x the throughput of 2 (256 registers, the tower temporaries spill) on the
 // full C3-BLS batch (profiles/r03_ab_bls_waves.jsonl)

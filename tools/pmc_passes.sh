@@ -1,15 +1,15 @@
 #!/bin/bash
 # rocprofv3 PMC passes over the C2 bench (one counter group per pass, as
 # MI355X_MICROARCH.md's rocprofv3 section prescribes).  Run on the GPU box:
-#   bash tools/pmc_passes.sh <outdir> [n]
+#   bash tools/pmc_passes.sh <outdir> [n] [extra bench.py args, e.g. --config c3bls]
 set -u
-out=${1:-gpurun_out/pmc}; n=${2:-1000000}
+out=${1:-gpurun_out/pmc}; n=${2:-1000000}; shift 2 2>/dev/null; extra=("$@")
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 run() {
   tag=$1; shift
   timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$out/$tag" -o pmc -- \
-    python3 bench.py --steps 1 --warmup 0 --n "$n" --no-cpu-baseline --no-e2e > "$out/$tag.log" 2>&1
+    python3 bench.py --steps 1 --warmup 0 --n "$n" --no-cpu-baseline --no-e2e "${extra[@]}" > "$out/$tag.log" 2>&1
   rc=$?
   echo "pass $tag rc=$rc"
   return $rc
