@@ -14,6 +14,10 @@
 static uint64_t g_cnt[2];
 static int g_bad = 0;
 static double g_max_col = 0;   // log2 of the largest |column sum| seen
+// the operand contract of bn::mul (pv_bn254.h f2mul): every limb below 2^30 and
+// at least one operand with every limb below 2^29 -- then NO arrangement of such
+// limbs can push a column past 2^62.3, whatever the values seen here
+static int g_disc_bad = 0;
 
 #define PV_HD static inline
 #define PV_BN_COUNT(kind) (++g_cnt[kind])
@@ -28,6 +32,16 @@ static void bn_check_mul(const int32_t* a, const int32_t* b);
 // |a_i| |b_j| summed per column (upper bound of the signed sum) + the
 // reduction products m_i p_j (< 2^28 * 2^28) + the carry in: < 2^63
 static void bn_check_mul(const int32_t* a, const int32_t* b) {
+  int64_t ma = 0, mb = 0;
+  for (int i = 0; i < bn::NL; ++i) {
+    const int64_t x = a[i] < 0 ? -(int64_t)a[i] : a[i], y = b[i] < 0 ? -(int64_t)b[i] : b[i];
+    ma = x > ma ? x : ma;
+    mb = y > mb ? y : mb;
+  }
+  if (ma >= (1ll << 30) || mb >= (1ll << 30) || (ma >= (1ll << 29) && mb >= (1ll << 29))) {
+    if (!g_disc_bad) fprintf(stderr, "bn254 operand contract violated: max limbs 2^%.2f, 2^%.2f\n", log2((double)ma), log2((double)mb));
+    g_disc_bad = 1;
+  }
   for (int k = 0; k < 2 * bn::NL - 1; ++k) {
     unsigned __int128 s = (unsigned __int128)1 << 36;   // carry
     for (int i = 0; i < bn::NL; ++i) {
@@ -51,6 +65,7 @@ using namespace bn;
 extern "C" {
 
 int bnc_bad(void) { return g_bad; }
+int bnc_disc_bad(void) { return g_disc_bad; }
 double bnc_max_col(void) { return g_max_col; }
 void bnc_counts(uint64_t* out) {
   out[0] = g_cnt[0];
@@ -59,6 +74,7 @@ void bnc_counts(uint64_t* out) {
 void bnc_reset(void) {
   g_cnt[0] = g_cnt[1] = 0;
   g_bad = 0;
+  g_disc_bad = 0;
   g_max_col = 0;
 }
 
