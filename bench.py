@@ -56,7 +56,7 @@ CONFIGS = {
 # Algorithmic work of the curve kernel per verify, counted by the host
 # instrumentation build of the same code (tests/test_hostcheck.py pins these):
 # field multiplies x 100 + squarings x 55 v_mad_u64_u32 (radix 2^25.5 schoolbook).
-# Generic batches (PV_CURVE_MODE=half, the default): half-size scalars, 128
+# Generic batches (curve_mode PV_CURVE_HALF, the default): half-size scalars, 128
 # doublings; decompression of -A and -R (each multiplies by sqrt(-1) for about
 # half of all points: the mean is a whole number of multiplies), two 9-entry
 # tables, 33 windows, identity test instead of an inversion.  Deferred records
@@ -68,7 +68,7 @@ W_SQ_PER_VERIFY = 1022.0
 W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
 W_MUL_FULL, W_SQ_FULL = 1587.5, 1517.0
 W_MAD_FULL = int(W_MUL_FULL * 100 + W_SQ_FULL * 55)
-# PV_CURVE_MODE=grouped: full-length scalars, CURVE_K = 4 signatures per lane
+# curve_mode PV_CURVE_GROUPED: full-length scalars, CURVE_K = 4 signatures per lane
 # sharing one inversion (3 of every 4 254-squaring inversions become 3 multiplies)
 W_MUL_GROUPED, W_SQ_GROUPED = 1581.5, 1326.5
 W_MAD_GROUPED = int(W_MUL_GROUPED * 100 + W_SQ_GROUPED * 55)
@@ -117,14 +117,22 @@ def _mad_peak():
         return P_MAD_PER_S
 
 
-def _traffic_per_launch():
-    """HBM bytes per curve launch from the committed rocprofv3 PMC summary, or None."""
-    path = os.path.join(REPO, 'profiles', 'r02_curve_pmc.json')
+TUNED = {}   # pv_tuning fields set from PV_* variables (main)
+CURVE_PMC = os.path.join(REPO, 'profiles', 'r04_curve_pmc.json')   # tools/gpu_pmc_r04.sh on the round-4 build
+BLS_PMC = os.path.join(REPO, 'profiles', 'r04_bls_pmc.json')
+
+
+def _pmc(path, key):
     try:
         with open(path) as fh:
-            return json.load(fh).get('hbm_bytes_per_launch')
+            return json.load(fh).get(key)
     except (OSError, ValueError):
         return None
+
+
+def _traffic_per_launch():
+    """HBM bytes per C2 curve launch from the committed rocprofv3 PMC summary, or None."""
+    return _pmc(CURVE_PMC, 'hbm_bytes_per_launch')
 
 
 # SURVEY.md 8(d)'s second work term, W_valu, ALGORITHMIC (VERDICT r2 weak #4):
@@ -137,14 +145,12 @@ def _traffic_per_launch():
 #            x19 wrap -> 20 half-rate; 5 x 2 f_odd + 10 masks + 2 adds -> 17 full-rate
 #   fe_sq    5 x 19 f + 10 carries + wrap -> 16 half; 9 x 2 f + 10 masks + 2 -> 21 full
 #   fe_add   10 full; fe_sub / fe_neg 20 full (+2p, -g); fe_carry 30 full (shift, mask, add)
-#   SHA-512  per block 80 rounds x 27 (12 v_alignbit, 8 v_bitop3, 7 64-bit adds)
-#            + 64 schedule words x 19 = 3376 half-rate
+# Only work the timed kernel (k_curve_half) does is charged: the SHA-512 of
+# R||A||M runs in k_hash, before it.
 W_ADD_PER_VERIFY, W_SUB_PER_VERIFY, W_CARRY_PER_VERIFY = 723, 778, 164
-SHA512_BLOCKS_C2 = 3          # |R||A||M| = 320 B
-HALF_COST = {'mul': 20, 'sq': 16, 'sha_block': 3376}
+HALF_COST = {'mul': 20, 'sq': 16}
 FULL_COST = {'mul': 17, 'sq': 21, 'add': 10, 'sub': 20, 'carry': 30}
-W_HALF_PER_VERIFY = (HALF_COST['mul'] * W_MUL_PER_VERIFY + HALF_COST['sq'] * W_SQ_PER_VERIFY
-                     + HALF_COST['sha_block'] * SHA512_BLOCKS_C2)
+W_HALF_PER_VERIFY = HALF_COST['mul'] * W_MUL_PER_VERIFY + HALF_COST['sq'] * W_SQ_PER_VERIFY
 W_FULL_PER_VERIFY = (FULL_COST['mul'] * W_MUL_PER_VERIFY + FULL_COST['sq'] * W_SQ_PER_VERIFY
                      + FULL_COST['add'] * W_ADD_PER_VERIFY + FULL_COST['sub'] * W_SUB_PER_VERIFY
                      + FULL_COST['carry'] * W_CARRY_PER_VERIFY)
@@ -170,7 +176,7 @@ def _combined_issue(kernel_rate, peak):
     (constants above, pinned by host op counts) and every P measured (the MAD
     ceiling; the other two classes at their measured ratios to it).  Beside it,
     `issue_efficiency` prices the instructions the kernel actually EXECUTES
-    (rocprofv3 SQ_INSTS_VALU, profiles/r02_curve_pmc.json) the same way."""
+    (rocprofv3 SQ_INSTS_VALU, profiles/r04_curve_pmc.json) the same way."""
     try:
         p_half, p_full = _class_rates(peak)
     except (OSError, KeyError, ValueError):
@@ -185,8 +191,7 @@ def _combined_issue(kernel_rate, peak):
            'source': 'W from tools/hostcheck op counters x per-primitive costs (bench.py); '
                      'P ratios from profiles/r01_int_rates.json'}
     try:
-        path = os.path.join(REPO, 'profiles', 'r02_curve_pmc.json')
-        with open(path) as fh:
+        with open(CURVE_PMC) as fh:
             d = json.load(fh)
         insts = float(d['kernels'][d['curve_kernel']]['SQ_INSTS_VALU'])
         n, deferred = int(d['c2_signatures']), int(d['c2_deferred'])
@@ -197,7 +202,7 @@ def _combined_issue(kernel_rate, peak):
         rate_exec = 1.0 / (W_MAD_PER_VERIFY / peak + other / p_half)
         out['issue_efficiency'] = {'executed_non_mad_per_verify': round(other), 'rate_at_executed_work': round(rate_exec, 1),
                                    'frac': round(kernel_rate / rate_exec, 4),
-                                   'source': 'rocprofv3 SQ_INSTS_VALU of the C2 curve launch (profiles/r02_curve_pmc.json)'}
+                                   'source': 'rocprofv3 SQ_INSTS_VALU of the C2 curve launch (profiles/r04_curve_pmc.json)'}
     except (OSError, KeyError, ValueError):
         pass
     return out
@@ -434,6 +439,8 @@ def main_c1(args):
             'sample': '{} requests (3 s) through the same CoreAuthNr.authenticate path one request at a time, '
                       'verification by libsodium 1.0.18 crypto_sign_open on 1 host thread (the node verifies on its '
                       'single Looper thread)'.format(done)}
+    if TUNED:
+        res['tuning'] = dict(TUNED)
     print(json.dumps(res), flush=True)
     return 0 if mism == 0 else 3
 
@@ -533,7 +540,11 @@ def main_bls(args):
         'kernel_ms': {'hash': round(hash_ms, 3), 'verify': round(verify_ms, 3)},
         'roofline': {'bound': 'valu', 'kernel': 'k_bls_verify', 'achieved': round(achieved / 1e12, 3),
                      'peak': round(peak / 1e12, 3), 'unit': 'T v_mad lane-ops/s', 'frac': round(achieved / peak, 4),
-                     'work_per_check': BLS_W_MAD, 'traffic': None,
+                     'work_per_check': BLS_W_MAD,
+                     'traffic': (round(_pmc(BLS_PMC, 'hbm_bytes_per_unit') * n, 1)
+                                 if _pmc(BLS_PMC, 'hbm_bytes_per_unit') else None),
+                     'traffic_source': 'HBM bytes per check from rocprofv3 FETCH_SIZE / WRITE_SIZE passes '
+                                       '(profiles/r04_bls_pmc.json) x the checks of this launch',
                      'note': 'W = {} Fp mul x 180 + {} sqr x 135 v_mad_i64_i32 per check (host op counts)'
                              .format(BLS_W_MUL, BLS_W_SQR)},
     }
@@ -573,6 +584,8 @@ def main_bls(args):
                                'sample': '{} checks of this workload, oracle/bn254_oracle.c (2 pairings per check, '
                                          'as ursa) on {} host threads'.format(sample, threads),
                                'agrees_with_gpu': bool((res.astype(bool) == got[:sample].cpu().numpy()).all())}
+    if TUNED:
+        out['tuning'] = dict(TUNED)
     print(json.dumps(out), flush=True)
 
 
@@ -712,6 +725,8 @@ def main_f3(args):
                          'sample': 'hashlib SHA-256 tree hash (the reference TreeHasher algorithm, level-wise) over '
                                    'the first {} leaves on 1 host thread'.format(sample)},
     }
+    if TUNED:
+        res['tuning'] = dict(TUNED)
     print(json.dumps(res), flush=True)
     return 0 if mism == 0 else 3
 
@@ -735,6 +750,10 @@ def main():
                     help='one stream, each step after the previous one (default: consecutive steps alternate over '
                          'two streams and two workspaces, so step k + 1 starts while step k\'s curve grid drains)')
     args = ap.parse_args()
+    # PV_* schedule knobs (A/B runs of tools/*.sh): an explicit opt-in here --
+    # the library never reads the environment; a non-default setting is
+    # reported in the line
+    TUNED.update(nat.tuning_from_env())
     if args.config == 'c1':
         return main_c1(args)
     if args.config == 'c3bls':
@@ -984,6 +1003,8 @@ def main():
         out['small_batch_latency'] = small_batch_latency(batch)
         mism += out['small_batch_latency']['verdict_mismatches']
     if rank == 0:
+        if TUNED:
+            out['tuning'] = dict(TUNED)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

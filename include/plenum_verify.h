@@ -282,57 +282,94 @@ int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *
                           uint64_t n, uint8_t *verdict, uint64_t *bitmap, int device, void *stream, int iters,
                           float *ms_hash, float *ms_curve);
 
-/* Curve-stage schedule of generic (non-keyed) batches on `device`, chosen by
- * the environment variable PV_CURVE_MODE at pv_init:
- *   PV_CURVE_HALF     (default, "half") half-size scalars: Euclid on (8L, h)
- *                     gives c == d h (mod 8L) with |c|, d < 2^131, d odd, and the
- *                     verdict is  s'B + c(-A) + d(-R) == O  (s' = dS mod L): the
- *                     same accept/reject as libsodium's encode(SB - hA) == R for
- *                     every input (derivation in indy-plenum_amd/csrc/pv_lattice.h);
- *                     the ~0.2 % of signatures whose h has no such (c, d) get the
- *                     full-length verdict in the same launch;
- *   PV_CURVE_FULL     ("full") every signature through the full-length verdict;
- *   PV_CURVE_GROUPED  ("grouped") the full-length kernel with 4 signatures per
- *                     lane sharing one inversion.
- * pv_set_curve_mode switches every initialised device (A/B timing, tests).
- * deferred (may be NULL) = signatures of the last generic batch on this device
- * that took the full-length verdict (0 if none ran). */
+/* ------------------------------------------------------------------------
+ * Schedule tuning.  pv_init reads NO environment: a node runs the defaults
+ * below unless its code calls pv_set_tuning.  None of these knobs changes a
+ * verdict (tests/test_gpu_verify.py and test_gpu_device.py run the fixtures
+ * through every setting); they exist for A/B timing (tools/) and tests.
+ *
+ *   curve_mode      curve stage of generic (non-keyed) batches:
+ *     PV_CURVE_HALF     (default) half-size scalars: Euclid on (8L, h) gives
+ *                       c == d h (mod 8L) with |c|, d < 2^131, d odd, and the
+ *                       verdict is  s'B + c(-A) + d(-R) == O  (s' = dS mod L): the
+ *                       same accept/reject as libsodium's encode(SB - hA) == R for
+ *                       every input (derivation in indy-plenum_amd/csrc/pv_lattice.h);
+ *                       the ~0.2 % of signatures whose h has no such (c, d) get the
+ *                       full-length verdict in the same launch;
+ *     PV_CURVE_FULL     every signature through the full-length verdict;
+ *     PV_CURVE_GROUPED  the full-length kernel, 4 signatures per lane sharing one
+ *                       inversion.
+ *   lat_max         generic batches of at most this many signatures (per device
+ *                   call / host-buffer shard) run the latency kernel: 8 lanes per
+ *                   signature (lane-pair split, each side's point over a lane
+ *                   QUAD, one coordinate per lane, DPP exchanges), so small
+ *                   batches finish ~2x sooner.  Default 32768 (the measured
+ *                   crossover with the throughput path is 32k-64k); 0 disables;
+ *                   at most 2^20.
+ *   lat_keyed_max   keyed batches (prepared keys, the key cache) of at most this
+ *                   many signatures run the keyed latency kernel (the key's comb
+ *                   over two lane quads per signature).  Default 8192; 0 disables.
+ *   lat_kernel      PV_LAT_QUAD (default) or PV_LAT_PAIR (the lane-pair kernel, A/B).
+ *   small_zc_max    host calls of at most this many signatures read their inputs
+ *                   from, and write verdicts to, mapped page-locked memory (no
+ *                   copies).  Default 2048; 0 = always copy.
+ *   host_fused      host-buffer chunks of generic batches: 1 (default) = one
+ *                   fused launch per chunk + one lane-quad pass over the deferred
+ *                   records; 0 = hash, lattice, curve launches per chunk.
+ *   host_staging    PV_STAGING_PINNED (default): each chunk is gathered by up to
+ *                   host_copy_threads host threads into one of two page-locked
+ *                   slots per device (at most host_pin_max_mb each) and DMA'd from
+ *                   there; PV_STAGING_PAGEABLE: the caller's buffers go straight
+ *                   to hipMemcpyAsync.  Switching to pageable releases the slots.
+ *   host_chunks     a shard runs as leading ramp chunks (host_ramp, 2 host_ramp,
+ *                   ... signatures below a regular chunk; host_ramp 0 = one first
+ *                   chunk of host_first_pct % of a regular one) and then about
+ *                   host_chunks equal chunks of >= 32768 signatures.
+ *                   Defaults 8 (1..256), ramp 32768 (0 or 1024..2^20),
+ *                   first_pct 50 (10..100), copy threads 8 (1..64), pin 512 MB
+ *                   (16..4096).
+ *   host_trace      1 = per-chunk host timings of pv_verify_batch on stderr.
+ *   test_dup_devices  TEST ONLY, read by the next pv_init: 2..8 opens that many
+ *                   engine devices, all on HIP device 0, so the multi-device
+ *                   paths (a worker thread per device, shard offsets, error
+ *                   aggregation) run on a one-GPU box; 0 (default) = one engine
+ *                   device per HIP device.
+ * pv_get_tuning fills *t with the current values (struct_size must be set to
+ * sizeof(pv_tuning) by the caller); pv_set_tuning validates every field
+ * (PV_EINVAL and nothing changes if one is out of range), keeps them for later
+ * pv_init calls and applies them to every initialised device.
+ * ---------------------------------------------------------------------- */
 #define PV_CURVE_HALF 0u
 #define PV_CURVE_FULL 1u
 #define PV_CURVE_GROUPED 2u
-int pv_set_curve_mode(uint32_t mode);
-
-/* Latency mode of the half-size path: generic batches of at most
- * max_signatures signatures (per device call / host-buffer chunk) run the
- * curve stage on 8 lanes per signature -- the lane-pair split (one side holds
- * A and the low half of s'B, the other R and the high half; they add their
- * points at the end), each side's point spread over a lane QUAD (one
- * coordinate per lane, DPP exchanges), so a doubling costs each lane one
- * squaring + one multiply: small batches, where a few waves occupy the GPU,
- * finish ~2x sooner.  Deferred records run in the same kernel.  Larger
- * batches keep the one-lane-per-signature throughput kernel.  Verdicts are
- * identical.  Default 32768 (the measured crossover with the throughput path
- * is between 32k and 64k signatures), env PV_LAT_MAX at pv_init; 0 disables. */
-int pv_set_lat_max(uint64_t max_signatures);
-/* Keyed batches (prepared keys: pv_verify_keyed_device, the key cache below)
- * of at most max_signatures signatures run the keyed latency kernel: the comb
- * of the prepared key split over two lane quads per signature (28 doublings
- * and 40 affine adds per lane) while one lane per signature hashes, -R decoded
- * beside the hash, one launch.  Verdicts are identical.  Default 8192, env
- * PV_LAT_KEYED_MAX at pv_init; 0 disables (the keyed throughput kernel). */
-int pv_set_lat_keyed_max(uint64_t max_signatures);
-/* Latency kernel: PV_LAT_QUAD (default, lane quads per point) or PV_LAT_PAIR
- * (the previous lane-pair kernel, one lane per point; A/B).  Env
- * PV_LAT_KERNEL=quad|pair at pv_init. */
 #define PV_LAT_QUAD 0u
 #define PV_LAT_PAIR 1u
-int pv_set_lat_kernel(uint32_t kernel);
-/* Host-buffer chunks of generic batches above the latency size: 1 (default) =
- * one fused launch per chunk (pre-checks + hash + scalar stage + half-size
- * curve per 64-signature task) and one lane-quad pass over the deferred
- * records; 0 = the device-resident schedule (hash, lattice, curve launches)
- * per chunk.  Same verdicts.  Env PV_HOST_FUSED=0|1 at pv_init. */
-int pv_set_host_fused(int enable);
+#define PV_STAGING_PINNED 0u
+#define PV_STAGING_PAGEABLE 1u
+typedef struct pv_tuning {
+  uint32_t struct_size;       /* sizeof(pv_tuning) */
+  uint32_t curve_mode;
+  uint64_t lat_max;
+  uint64_t lat_keyed_max;
+  uint64_t small_zc_max;
+  uint32_t lat_kernel;
+  uint32_t host_fused;
+  uint32_t host_staging;
+  uint32_t host_chunks;
+  uint32_t host_first_pct;
+  uint32_t host_copy_threads;
+  uint64_t host_ramp;
+  uint32_t host_pin_max_mb;
+  uint32_t host_trace;
+  uint32_t test_dup_devices;
+  uint32_t reserved;
+} pv_tuning;
+int pv_get_tuning(pv_tuning *t);
+int pv_set_tuning(const pv_tuning *t);
+
+/* mode (may be NULL) = the curve_mode of `device`; deferred (may be NULL) =
+ * signatures of the last generic batch on this device that took the
+ * full-length verdict (0 if none ran). */
 int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
 
 /* Live kernel timing of the verify calls themselves (bench.py's timed region):
@@ -349,27 +386,7 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
                                 uint64_t *bitmap, int device, void *stream, int iters, float *ms_hash,
                                 float *ms_curve);
 
-/* Host-side staging of pv_verify_batch's inputs, chosen by PV_HOST_STAGING /
- * PV_HOST_COPY_THREADS / PV_HOST_CHUNKS at pv_init.  A shard runs as a
- * pipeline of chunks: short leading chunks (32768, 65536, ... signatures below
- * a regular chunk; PV_HOST_RAMP env, 0 = one first chunk of PV_HOST_FIRST_PCT %
- * of a regular one) so the kernels start early, then about `chunks` equal
- * chunks of >= 32768 signatures.
- *   PV_STAGING_PINNED   ("pinned", default) each chunk is gathered by up to
- *                       copy_threads host threads into one of two page-locked
- *                       slots per device and DMA'd from there; verdicts come
- *                       back through a page-locked buffer;
- *   PV_STAGING_PAGEABLE ("pageable") the caller's buffers go straight to
- *                       hipMemcpyAsync (the runtime stages them).
- * Verdicts are identical either way.  pv_set_host_staging switches every
- * initialised device (A/B timing, tests); copy_threads / chunks 0 keep the
- * current value, otherwise 1..64 / 1..256.  Switching to pageable releases the
- * page-locked slots; with pinned staging each device holds at most two slots of
- * PV_HOST_PIN_MAX_MB (env, default 512) plus one byte per signature of its
- * largest shard. */
-#define PV_STAGING_PINNED 0u
-#define PV_STAGING_PAGEABLE 1u
-int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks);
+
 
 
 /* ------------------------------------------------------------------------
@@ -422,7 +439,9 @@ int pv_bls_verify_batch(const uint8_t *sig, const uint64_t *sig_len, const uint8
                         uint64_t n_msgs, const uint32_t *msg_idx, const uint32_t *key_idx, uint64_t n,
                         uint8_t *verdict, int device);
 /* Same with DEVICE pointers (msg_blob needs >= 16 readable bytes past the last
- * message); synchronous on `stream` (NULL = library stream). */
+ * message); synchronous on `stream` (NULL = library stream).  Indices are not
+ * checked on the host here: a check whose key_idx is >= the key count or whose
+ * msg_idx is >= n_msgs is skipped by the kernels and gets verdict 0. */
 int pv_bls_verify_batch_device(const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n_msgs,
                                const uint32_t *msg_idx, const uint32_t *key_idx, uint64_t n, uint8_t *verdict,
                                int device, void *stream);
@@ -433,6 +452,28 @@ int pv_bls_sign_batch(const uint8_t *sks, uint64_t k, const uint8_t *msg_blob, c
 int pv_bls_sign_batch_device(const uint8_t *sks, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n_msgs,
                              const uint32_t *msg_idx, const uint32_t *key_idx, uint64_t n, uint8_t *sig, int device,
                              void *stream);
+/* n multi-signature checks from HOST memory; replaces n calls of
+ *   BlsCryptoVerifierIndyCrypto.verify_multi_sig(signature, message, pks)
+ *   (crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:84-97), made once per
+ *   ledger of every PRE-PREPARE by BlsBftReplicaPlenum._validate_multi_sig
+ *   (plenum/bls/bls_bft_replica_plenum.py:43-50, 212-225), i.e. python-ursa
+ *   Bls.verify_multi_sig: e(sigma, g) == e(H(msg), sum of the keys).
+ * Check j: sig[j] (128 B; sig_len as in pv_bls_verify_batch), message
+ * msg_idx[j] of msg_blob/msg_off, keys pks[pk_off[j] .. pk_off[j+1]) (128 B each,
+ * decoded as keys are; an empty set sums to O).  The sum is prepared like a key
+ * (PV_BLS_KEY_NOT_IN_G2 -> verdict 0) together with the generator `gen`; the key
+ * set of pv_bls_set_keys is not touched.  At most 65535 checks per call. */
+int pv_bls_verify_multi_batch(const uint8_t *gen, const uint8_t *sig, const uint64_t *sig_len, const uint8_t *msg_blob,
+                              const uint64_t *msg_off, uint64_t n_msgs, const uint32_t *msg_idx, const uint8_t *pks,
+                              const uint64_t *pk_off, uint64_t n, uint8_t *verdict, int device);
+/* m multi-signatures; replaces m calls of
+ *   BlsCryptoVerifierIndyCrypto.create_multi_sig(signatures) (:99-102), made by
+ *   BlsBftReplicaPlenum._calculate_single_multi_sig (bls_bft_replica_plenum.py:278-288),
+ *   i.e. python-ursa MultiSignature.new: the sum of the signatures' G1 points.
+ * Set j = sigs[set_off[j] .. set_off[j+1]) (128 B each, decoded as sigma is);
+ * out[j] = the sum's 128-byte representation: 0x04|x|y, zero-padded; the point
+ * at infinity as 0x04|0|1 (AMCL's affine (0, 1) of O). */
+int pv_bls_aggregate_sigs(const uint8_t *sigs, const uint64_t *set_off, uint64_t m, uint8_t *out, int device);
 /* pks[i] = sks[i] * gen (k keys, 128 B each) */
 int pv_bls_pubkeys(const uint8_t *gen, const uint8_t *sks, uint64_t k, uint8_t *pks, int device);
 /* HIP-event durations of the last verify call on `device`: message hashing and the check kernel */

@@ -53,20 +53,20 @@ int fail(int code, const char* fmt, ...) {
 // fused chunks 11.6 vs 12.1 ms, profiles/r02_ab_fused_chunking.jsonl)
 #define PV_HOST_RAMP 32768
 // generic batches of at most this many signatures run the latency-mode curve
-// kernel (k_verify_quad: one launch, lane quads per point); PV_LAT_MAX env overrides (0 disables)
+// kernel (k_verify_quad: one launch, lane quads per point); tuning.lat_max (0 disables)
 #define PV_LAT_MAX 32768
 // keyed batches (prepared keys) of at most this many signatures run the keyed
-// latency kernel (k_verify_quad_keyed); PV_LAT_KEYED_MAX env overrides (0 disables)
+// latency kernel (k_verify_quad_keyed); tuning.lat_keyed_max (0 disables)
 #define PV_LAT_KEYED_MAX 8192
 // host-buffer calls of at most this many signatures skip the H2D / D2H copies:
 // the latency kernel reads the gathered inputs from, and writes the verdicts
 // to, fine-grained page-locked host memory (one launch per call instead of
-// copy + launch + copy); PV_SMALL_ZC_MAX env overrides (0 = always copy)
+// copy + launch + copy); tuning.small_zc_max (0 = always copy)
 #define PV_SMALL_ZC_MAX 2048
 // shards of at least this many signatures decide PV_FLAG_DEDUP_KEYS from a sample
 #define PV_DEDUP_SAMPLE_MIN 262144
 // chunk gathers into the pinned staging ring use up to this many host threads
-// (PV_HOST_COPY_THREADS overrides); gathers under PV_HOST_PAR_MIN bytes stay on
+// (tuning.host_copy_threads); gathers under PV_HOST_PAR_MIN bytes stay on
 // the calling thread
 #define PV_HOST_COPY_THREADS 8
 #define PV_HOST_PAR_MIN (4u << 20)
@@ -395,24 +395,24 @@ struct Device {
   hipStream_t stream = nullptr;
   hipStream_t copy = nullptr;   // host-buffer calls: H2D of chunk c+1 overlaps the kernels of chunk c
   hipEvent_t copied = nullptr;  // recorded on `copy` after each chunk's inputs, waited on by `stream`
-  // PV_HOST_STAGING (read at pv_init): "pinned" (default) gathers chunk c of a
+  // tuning.host_staging: PV_STAGING_PINNED (default) gathers chunk c of a
   // host-buffer call into page-locked slot c & 1 and DMAs it from there;
-  // "pageable" hands the caller's buffers to hipMemcpyAsync (runtime staging)
+  // PV_STAGING_PAGEABLE hands the caller's buffers to hipMemcpyAsync (runtime staging)
   bool pinned = true;
   int copy_threads = PV_HOST_COPY_THREADS;
-  int host_chunks = PV_HOST_CHUNKS;  // PV_HOST_CHUNKS env overrides (1..256)
-  int first_pct = 50;                // first chunk, % of a regular one; PV_HOST_FIRST_PCT env (10..100)
+  int host_chunks = PV_HOST_CHUNKS;  // tuning.host_chunks (1..256)
+  int first_pct = 50;                // first chunk, % of a regular one; tuning.host_first_pct (10..100)
   // leading chunks r, 2r, 4r, ... below a regular chunk instead of one first
-  // chunk (PV_HOST_RAMP env; 0 = off, first_pct then sizes the first chunk)
+  // chunk (tuning.host_ramp; 0 = off, first_pct then sizes the first chunk)
   uint64_t ramp = PV_HOST_RAMP;
-  size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; PV_HOST_PIN_MAX_MB env overrides (16..4096)
-  uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; PV_LAT_MAX env (0 = off)
+  size_t pin_max = PV_HOST_PIN_MAX;  // largest page-locked slot; tuning.host_pin_max_mb (16..4096)
+  uint64_t lat_max = PV_LAT_MAX;     // generic batches up to this size use the latency kernel; tuning.lat_max (0 = off)
   uint64_t lat_keyed_max = PV_LAT_KEYED_MAX;  // keyed batches up to this size: k_verify_quad_keyed
-  uint64_t zc_max = PV_SMALL_ZC_MAX;          // host calls up to this size: zero-copy (PV_SMALL_ZC_MAX env)
+  uint64_t zc_max = PV_SMALL_ZC_MAX;          // host calls up to this size: zero-copy (tuning.small_zc_max)
   PinBuf zc_in, zc_out;                       // fine-grained page-locked image / verdicts of zero-copy calls
-  bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_KERNEL=pair: k_curve_lat
+  bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_PAIR: k_curve_lat
   // host-buffer chunks of generic batches: one k_chunk_half launch per chunk
-  // + one k_verify_quad_list pass for the deferred records; PV_HOST_FUSED=0:
+  // + one k_verify_quad_list pass for the deferred records; tuning.host_fused 0:
   // k_hash + k_lattice + k_curve_half per chunk (the device-resident schedule)
   bool chunk_fused = true;
   DevBuf<uint32_t> dl;               // shard indices deferred by k_chunk_half
@@ -483,6 +483,74 @@ Device* find_dev(int id) {
   return nullptr;
 }
 
+// the process's schedule tuning (include/plenum_verify.h, pv_set_tuning):
+// defaults only, never the environment
+pv_tuning default_tuning() {
+  pv_tuning t{};
+  t.struct_size = sizeof(pv_tuning);
+  t.curve_mode = PV_CURVE_HALF;
+  t.lat_max = PV_LAT_MAX;
+  t.lat_keyed_max = PV_LAT_KEYED_MAX;
+  t.small_zc_max = PV_SMALL_ZC_MAX;
+  t.lat_kernel = PV_LAT_QUAD;
+  t.host_fused = 1;
+  t.host_staging = PV_STAGING_PINNED;
+  t.host_chunks = PV_HOST_CHUNKS;
+  t.host_first_pct = 50;
+  t.host_copy_threads = PV_HOST_COPY_THREADS;
+  t.host_ramp = PV_HOST_RAMP;
+  t.host_pin_max_mb = (uint32_t)(PV_HOST_PIN_MAX >> 20);
+  return t;
+}
+pv_tuning g_tune = default_tuning();
+
+int check_tuning(const pv_tuning& t) {
+  if (t.struct_size != sizeof(pv_tuning))
+    return fail(PV_EINVAL, "struct_size %u != sizeof(pv_tuning) %zu", t.struct_size, sizeof(pv_tuning));
+  if (t.curve_mode > PV_CURVE_GROUPED) return fail(PV_EINVAL, "unknown curve mode %u", t.curve_mode);
+  if (t.lat_max > (1ull << 20) || t.lat_keyed_max > (1ull << 20) || t.small_zc_max > (1ull << 20))
+    return fail(PV_EINVAL, "lat_max / lat_keyed_max / small_zc_max must be <= 2^20");
+  if (t.lat_kernel > PV_LAT_PAIR) return fail(PV_EINVAL, "unknown latency kernel %u", t.lat_kernel);
+  if (t.host_fused > 1) return fail(PV_EINVAL, "host_fused must be 0 or 1");
+  if (t.host_staging > PV_STAGING_PAGEABLE) return fail(PV_EINVAL, "unknown staging mode %u", t.host_staging);
+  if (t.host_chunks < 1 || t.host_chunks > 256) return fail(PV_EINVAL, "host_chunks must be in 1..256");
+  if (t.host_first_pct < 10 || t.host_first_pct > 100) return fail(PV_EINVAL, "host_first_pct must be in 10..100");
+  if (t.host_copy_threads < 1 || t.host_copy_threads > 64) return fail(PV_EINVAL, "host_copy_threads must be in 1..64");
+  if (t.host_ramp != 0 && (t.host_ramp < 1024 || t.host_ramp > (1ull << 20)))
+    return fail(PV_EINVAL, "host_ramp must be 0 or in 1024..2^20");
+  if (t.host_pin_max_mb < 16 || t.host_pin_max_mb > 4096) return fail(PV_EINVAL, "host_pin_max_mb must be in 16..4096");
+  if (t.host_trace > 1) return fail(PV_EINVAL, "host_trace must be 0 or 1");
+  if (t.test_dup_devices == 1 || t.test_dup_devices > 8) return fail(PV_EINVAL, "test_dup_devices must be 0 or 2..8");
+  return PV_OK;
+}
+
+void apply_tuning(Device& d, const pv_tuning& t) {
+  const CurveMode m = t.curve_mode == PV_CURVE_HALF ? CurveMode::Half
+                      : t.curve_mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
+  if (m != d.mode)
+    for (auto& w : d.ws) w.half_ran = false;
+  d.mode = m;
+  d.lat_max = t.lat_max;
+  d.lat_keyed_max = t.lat_keyed_max;
+  d.zc_max = t.small_zc_max;
+  d.lat_quad = t.lat_kernel == PV_LAT_QUAD;
+  d.chunk_fused = t.host_fused != 0;
+  d.host_chunks = (int)t.host_chunks;
+  d.first_pct = (int)t.host_first_pct;
+  d.copy_threads = (int)t.host_copy_threads;
+  d.ramp = t.host_ramp;
+  d.pin_max = size_t(t.host_pin_max_mb) << 20;
+  const bool pinned = t.host_staging == PV_STAGING_PINNED;
+  if (d.pinned && !pinned && d.copy) {   // pageable staging holds no page-locked memory
+    (void)hipSetDevice(d.ord);
+    (void)hipStreamSynchronize(d.copy);
+    d.pin[0].release();
+    d.pin[1].release();
+    d.vout.release();
+  }
+  d.pinned = pinned;
+}
+
 int init_device(Device& d) {
   HIP_OK(hipSetDevice(d.ord));
   HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
@@ -494,58 +562,8 @@ int init_device(Device& d) {
   HIP_OK(hipEventCreateWithFlags(&d.keys_ready, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&d.joined, hipEventDisableTiming));
   for (auto& w : d.ws) HIP_OK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
-  if (const char* m = getenv("PV_HOST_STAGING")) {
-    if (!strcmp(m, "pageable")) d.pinned = false;
-    else if (strcmp(m, "pinned") != 0) return fail(PV_EINVAL, "PV_HOST_STAGING must be pinned or pageable (got %s)", m);
-  }
-  if (const char* t = getenv("PV_HOST_CHUNKS")) {
-    d.host_chunks = atoi(t);
-    if (d.host_chunks < 1 || d.host_chunks > 256) return fail(PV_EINVAL, "PV_HOST_CHUNKS must be in 1..256 (got %s)", t);
-  }
-  if (const char* t = getenv("PV_HOST_FIRST_PCT")) {
-    d.first_pct = atoi(t);
-    if (d.first_pct < 10 || d.first_pct > 100)
-      return fail(PV_EINVAL, "PV_HOST_FIRST_PCT must be in 10..100 (got %s)", t);
-  }
-  if (const char* t = getenv("PV_HOST_RAMP")) {
-    const long v = atol(t);
-    if (v != 0 && (v < 1024 || v > (1L << 20))) return fail(PV_EINVAL, "PV_HOST_RAMP must be 0 or in 1024..1048576 (got %s)", t);
-    d.ramp = (uint64_t)v;
-  }
-  if (const char* t = getenv("PV_LAT_MAX")) {
-    const long v = atol(t);
-    if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_MAX must be in 0..1048576 (got %s)", t);
-    d.lat_max = (uint64_t)v;
-  }
-  if (const char* t = getenv("PV_LAT_KEYED_MAX")) {
-    const long v = atol(t);
-    if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_LAT_KEYED_MAX must be in 0..1048576 (got %s)", t);
-    d.lat_keyed_max = (uint64_t)v;
-  }
-  if (const char* t = getenv("PV_SMALL_ZC_MAX")) {
-    const long v = atol(t);
-    if (v < 0 || v > (1L << 20)) return fail(PV_EINVAL, "PV_SMALL_ZC_MAX must be in 0..1048576 (got %s)", t);
-    d.zc_max = (uint64_t)v;
-  }
   d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped;
-  if (const char* t = getenv("PV_HOST_FUSED")) {
-    if (strcmp(t, "0") != 0 && strcmp(t, "1") != 0) return fail(PV_EINVAL, "PV_HOST_FUSED must be 0 or 1 (got %s)", t);
-    d.chunk_fused = t[0] == '1';
-  }
-  if (const char* m = getenv("PV_LAT_KERNEL")) {
-    if (!strcmp(m, "pair")) d.lat_quad = false;
-    else if (strcmp(m, "quad") != 0) return fail(PV_EINVAL, "PV_LAT_KERNEL must be quad or pair (got %s)", m);
-  }
-  if (const char* t = getenv("PV_HOST_PIN_MAX_MB")) {
-    const long mb = atol(t);
-    if (mb < 16 || mb > 4096) return fail(PV_EINVAL, "PV_HOST_PIN_MAX_MB must be in 16..4096 (got %s)", t);
-    d.pin_max = size_t(mb) << 20;
-  }
-  if (const char* t = getenv("PV_HOST_COPY_THREADS")) {
-    d.copy_threads = atoi(t);
-    if (d.copy_threads < 1 || d.copy_threads > 64)
-      return fail(PV_EINVAL, "PV_HOST_COPY_THREADS must be in 1..64 (got %s)", t);
-  }
+  apply_tuning(d, g_tune);
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d.ord));
   d.cu_count = prop.multiProcessorCount;
@@ -571,11 +589,6 @@ int init_device(Device& d) {
     HIP_OK(d.ws[0].scratch.ensure(d.scratch_words));
   }
   HIP_OK(d.ws[0].qc.ensure(2));
-  if (const char* m = getenv("PV_CURVE_MODE")) {
-    if (!strcmp(m, "full")) d.mode = CurveMode::Full;
-    else if (!strcmp(m, "grouped")) d.mode = CurveMode::Grouped;
-    else if (strcmp(m, "half") != 0) return fail(PV_EINVAL, "PV_CURVE_MODE must be half, full or grouped (got %s)", m);
-  }
   int kper = 0;
   HIP_OK(pv::curve_occupancy(&kper, true));
   if (kper < 1) kper = 1;
@@ -721,7 +734,7 @@ int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig
     w.half_ran = true;
     d.last_ws = (int)(&w - d.ws);
   } else if (half && n <= d.lat_max) {
-    // (PV_LAT_KERNEL=pair) lane pairs per signature, one table of scratch per lane
+    // (PV_LAT_PAIR) lane pairs per signature, one table of scratch per lane
     HIP_OK(w.scratch.ensure(std::max<size_t>(d.scratch_words, (size_t)((2 * n + 63) / 64 * 64) * pv::ATAB_LAT_WORDS)));
     HIP_OK(pv::launch_curve_lat(pk, sig, w.h.p, w.hrec.p, d.btab.p, d.bw.p, w.scratch.p,
                                 w.scratch.cap / pv::ATAB_LAT_WORDS, verdict, bm, n, s));
@@ -1011,7 +1024,7 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   HIP_OK(d.off.ensure(m + 1));
   HIP_OK(d.verdict.ensure(m));
   // chunk bounds: short leading chunks so the kernels start early -- the
-  // ramp r, 2r, ... below a regular chunk (default), or with PV_HOST_RAMP=0
+  // ramp r, 2r, ... below a regular chunk (default), or with host_ramp 0
   // one first chunk of first_pct % of a regular one (>= PV_HOST_CHUNK_MIN) --
   // then the rest in equal chunks.  With pinned
   // staging the chunk count doubles until a chunk's inputs fit one
@@ -1027,7 +1040,7 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     const uint64_t first = std::min(m, std::max<uint64_t>(PV_HOST_CHUNK_MIN, reg * (uint64_t)d.first_pct / 100));
     bounds.assign(1, 0);
     if (hc > 1 && d.ramp) {
-      // PV_HOST_RAMP=r: leading chunks of r, 2r, 4r, ... signatures (< a
+      // tuning.host_ramp = r: leading chunks of r, 2r, 4r, ... signatures (< a
       // regular chunk), so the first kernels start after a short DMA
       for (uint64_t r = d.ramp; r < reg && bounds.back() + r < m; r *= 2) bounds.push_back(bounds.back() + r);
     } else if (hc > 1 && first < m) {
@@ -1088,8 +1101,8 @@ int run_shard(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     HIP_OK(hipEventRecord(d.keys_ready, d.ws[0].stream));
     HIP_OK(hipStreamWaitEvent(d.ws[1].stream, d.keys_ready, 0));
   }
-  // PV_HOST_TRACE=1: per-chunk host timings on stderr (pipeline diagnostics)
-  static const bool trace = getenv("PV_HOST_TRACE") && getenv("PV_HOST_TRACE")[0] == '1';
+  // tuning.host_trace: per-chunk host timings on stderr (pipeline diagnostics)
+  const bool trace = g_tune.host_trace != 0;
   const auto tstart = std::chrono::steady_clock::now();
   auto us = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tstart).count(); };
   if (trace) fprintf(stderr, "[pv host] dev %d shard %llu sigs: setup %.1f us, %zu chunks, pinned %d, direct %d\n", d.id,
@@ -1237,15 +1250,10 @@ int pv_init(uint32_t device_mask) {
   int count = 0;
   hipError_t e = hipGetDeviceCount(&count);
   if (e != hipSuccess || count <= 0) return fail(PV_ENODEV, "no HIP device available (%s)", hipGetErrorString(e));
-  // PV_TEST_DUP_DEVICE=k (test only, 2..8): k engine devices 0..k-1 all on HIP
-  // device 0, so the multi-device paths (one worker thread per device, shard
-  // offsets, error aggregation) run on a one-GPU box
-  int dup = 0;
-  if (const char* t = getenv("PV_TEST_DUP_DEVICE")) {
-    dup = atoi(t);
-    if (dup == 1) dup = 2;
-    if (dup < 0 || dup > 8) return fail(PV_EINVAL, "PV_TEST_DUP_DEVICE must be in 0..8 (got %s)", t);
-  }
+  // tuning.test_dup_devices = k (test only, 2..8): k engine devices 0..k-1 all
+  // on HIP device 0, so the multi-device paths (one worker thread per device,
+  // shard offsets, error aggregation) run on a one-GPU box
+  const int dup = (int)g_tune.test_dup_devices;
   const int n_ids = dup ? dup : count;
   for (int id = 0; id < n_ids && id < 32; ++id) {
     if (device_mask && !((device_mask >> id) & 1u)) continue;
@@ -1627,67 +1635,25 @@ int pv_kernel_timing(int device, int enable, float* hash_ms, float* curve_ms, ui
   return PV_OK;
 }
 
-int pv_set_curve_mode(uint32_t mode) {
+int pv_get_tuning(pv_tuning* t) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
-  if (mode > PV_CURVE_GROUPED) return fail(PV_EINVAL, "unknown curve mode %u", mode);
-  for (auto& d : g_devs) {
-    d.mode = mode == PV_CURVE_HALF ? CurveMode::Half : mode == PV_CURVE_FULL ? CurveMode::Full : CurveMode::Grouped;
-    for (auto& w : d.ws) w.half_ran = false;
-  }
+  if (!t) return fail(PV_EINVAL, "null pointer");
+  if (t->struct_size != sizeof(pv_tuning))
+    return fail(PV_EINVAL, "struct_size %u != sizeof(pv_tuning) %zu", t->struct_size, sizeof(pv_tuning));
+  *t = g_tune;
   return PV_OK;
 }
 
-int pv_set_host_fused(int enable) {
+int pv_set_tuning(const pv_tuning* t) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
-  for (auto& d : g_devs) d.chunk_fused = enable != 0;
-  return PV_OK;
-}
-
-int pv_set_lat_kernel(uint32_t kernel) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
-  if (kernel > PV_LAT_PAIR) return fail(PV_EINVAL, "unknown latency kernel %u", kernel);
-  for (auto& d : g_devs) d.lat_quad = kernel == PV_LAT_QUAD;
-  return PV_OK;
-}
-
-int pv_set_lat_max(uint64_t max_signatures) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
-  if (max_signatures > (1ull << 20)) return fail(PV_EINVAL, "max_signatures must be <= 2^20");
-  for (auto& d : g_devs) d.lat_max = max_signatures;
-  return PV_OK;
-}
-
-int pv_set_lat_keyed_max(uint64_t max_signatures) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
-  if (max_signatures > (1ull << 20)) return fail(PV_EINVAL, "max_signatures must be <= 2^20");
-  for (auto& d : g_devs) d.lat_keyed_max = max_signatures;
-  return PV_OK;
-}
-
-int pv_set_host_staging(uint32_t mode, int copy_threads, int chunks) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (g_devs.empty()) return fail(PV_ENOTINIT, "pv_init has not been called");
-  if (mode > PV_STAGING_PAGEABLE) return fail(PV_EINVAL, "unknown staging mode %u", mode);
-  if (copy_threads < 0 || copy_threads > 64) return fail(PV_EINVAL, "copy_threads must be in 0..64 (got %d)", copy_threads);
-  if (chunks < 0 || chunks > 256) return fail(PV_EINVAL, "chunks must be in 0..256 (got %d)", chunks);
+  if (!t) return fail(PV_EINVAL, "null pointer");
+  if (int rc = check_tuning(*t)) return rc;
+  const bool dup_changed = t->test_dup_devices != g_tune.test_dup_devices;
+  if (dup_changed && !g_devs.empty())
+    return fail(PV_EINVAL, "test_dup_devices is read by pv_init: call pv_shutdown first");
+  g_tune = *t;
   DeviceGuard dg;
-  for (auto& d : g_devs) {
-    d.pinned = mode == PV_STAGING_PINNED;
-    if (copy_threads) d.copy_threads = copy_threads;
-    if (chunks) d.host_chunks = chunks;
-    if (!d.pinned) {  // pageable staging holds no page-locked memory
-      (void)hipSetDevice(d.ord);
-      (void)hipStreamSynchronize(d.copy);
-      d.pin[0].release();
-      d.pin[1].release();
-      d.vout.release();
-    }
-  }
+  for (auto& d : g_devs) apply_tuning(d, g_tune);
   return PV_OK;
 }
 

@@ -90,9 +90,10 @@ __global__ __launch_bounds__(64) void k_bls_hash(const uint8_t* __restrict__ blo
 }
 
 // grouping by key: count, padded segment starts (64-aligned), scatter
-__global__ void k_bls_count(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t* __restrict__ cnt) {
+// a check whose key index is out of range is never scheduled: its verdict stays 0
+__global__ void k_bls_count(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys, uint32_t* __restrict__ cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicAdd(cnt + key_idx[i], 1u);
+  if (i < n && key_idx[i] < nkeys) atomicAdd(cnt + key_idx[i], 1u);
 }
 
 __global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uint32_t* __restrict__ seg,
@@ -106,11 +107,13 @@ __global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uin
   *total = s;
 }
 
-__global__ void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, const uint32_t* __restrict__ seg,
-                              uint32_t* __restrict__ cursor, uint32_t* __restrict__ order) {
+__global__ void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
+                              const uint32_t* __restrict__ seg, uint32_t* __restrict__ cursor,
+                              uint32_t* __restrict__ order) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t key = key_idx[i];
+  if (key >= nkeys) return;
   order[seg[key] + atomicAdd(cursor + key, 1u)] = (uint32_t)i;
 }
 
@@ -119,7 +122,8 @@ __global__ void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, 
 __global__ __launch_bounds__(BLS_BLOCK, PV_BLS_WAVES) void k_bls_verify(
     const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
     const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
-    const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint8_t* __restrict__ verdict) {
+    const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint32_t n_msgs,
+    uint8_t* __restrict__ verdict) {
   const uint32_t slot = blockIdx.x * BLS_BLOCK + threadIdx.x;
   const uint32_t task0 = __builtin_amdgcn_readfirstlane(slot & ~63u);
   if (task0 >= *total) return;   // whole wave: past the last padded segment
@@ -132,16 +136,71 @@ __global__ __launch_bounds__(BLS_BLOCK, PV_BLS_WAVES) void k_bls_verify(
   const uint8_t st = kstatus[1 + key];
   fp xs, ys, xqh = fzero(), yqh = fzero();
   bool s_inf = true;
+  const bool msg_ok = live && msg_idx[j] < n_msgs;   // out of range: verdict 0
   if (live) {
     g1_decode(sig + 128ull * j, xs, ys, s_inf);
-    const uint32_t* t = msgtab + (uint64_t)MSG_WORDS * msg_idx[j];
-    if (st == 0) {
+    const uint32_t* t = msgtab + (uint64_t)MSG_WORDS * (msg_ok ? msg_idx[j] : 0u);
+    if (st == 0 && msg_ok) {
       xqh = ld_fp(t + 2 * NL);
       yqh = ld_fp(t + 3 * NL);
     }
   }
   const bool ok = bls_check(xs, ys, s_inf, xqh, yqh, st == 1, g_lines, pk_lines);
-  if (live) verdict[j] = (st == 2) ? 0 : (uint8_t)ok;
+  if (live) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
+}
+
+// Bls::verify_multi_sig's aggregated key (ursa: PointG2::new_inf() + every
+// ver_key.point): one lane per check sums its keys (each decoded as
+// ECP2::frombytes: off the twist = O) and writes the sum's 128-byte affine
+// representation at pts[1 + i]; O is written as 128 zero bytes, which decode off
+// the twist (0 != 2/(1+i)), i.e. back to O.  k_bls_lines then prepares the sums
+// like keys (status, subgroup check, lines).
+__global__ __launch_bounds__(64) void k_bls_agg_g2(const uint8_t* __restrict__ pks, const uint64_t* __restrict__ set_off,
+                                                   uint32_t m, uint8_t* __restrict__ pts) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  g2j acc{f2one(), f2one(), f2zero()};
+  for (uint64_t t = set_off[i]; t < set_off[i + 1]; ++t) {
+    g2a q;
+    if (g2_decode(pks + 128ull * t, q, false) != 0) continue;
+    acc = g2j_add(acc, g2j{q.x, q.y, f2one()});
+  }
+  uint8_t* out = pts + 128ull * (1 + i);
+  for (int b = 0; b < 128; ++b) out[b] = 0;
+  if (f2is_zero(acc.z)) return;
+  const fp2 zi = f2inv(acc.z), zi2 = f2sqr(zi);
+  const fp2 x = f2mul(acc.x, zi2), y = f2mul(acc.y, f2mul(zi2, zi));
+  to_be32(out, from_mont(x.a));
+  to_be32(out + 32, from_mont(x.b));
+  to_be32(out + 64, from_mont(y.a));
+  to_be32(out + 96, from_mont(y.b));
+}
+
+// MultiSignature::new (ursa: PointG1::new_inf() + every signature's point, each
+// decoded as ECP::frombytes) -> its 128-byte representation (ECP::tobytes,
+// uncompressed: 0x04|x|y; O as AMCL's (x, y) = (0, 1) of its infinity)
+__global__ __launch_bounds__(64) void k_bls_agg_g1(const uint8_t* __restrict__ sigs, const uint64_t* __restrict__ set_off,
+                                                   uint32_t m, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  g1j acc{fone(), fone(), fzero()};
+  bool inf = true;
+  for (uint64_t t = set_off[i]; t < set_off[i + 1]; ++t) {
+    fp x, y;
+    bool s_inf;
+    g1_decode(sigs + 128ull * t, x, y, s_inf);
+    if (!s_inf) acc = g1j_add_affine(acc, inf, x, y);
+  }
+  uint8_t* o = out + 128ull * i;
+  for (int b = 0; b < 128; ++b) o[b] = 0;
+  o[0] = 4;
+  if (inf || is_zero(acc.z)) {
+    o[64] = 1;
+    return;
+  }
+  const fp zi = inv(acc.z), zi2 = sqr(zi);
+  to_be32(o + 1, from_mont(mul(acc.x, zi2)));
+  to_be32(o + 33, from_mont(mul(acc.y, mul(zi2, zi))));
 }
 
 // data generation: sig[j] = sk[key_idx[j]] * H(msg_idx[j])
@@ -220,17 +279,30 @@ struct Buf {
   }
 };
 
+// a prepared set of G2 arguments: point 0 = the generator, points 1..nkeys the
+// keys (or, for multi-signature checks, the per-check aggregated keys)
+struct KeySet {
+  uint32_t nkeys = 0;             // lines of 1 + nkeys points are valid (0: no set)
+  Buf<uint32_t> lines;
+  Buf<uint8_t> kstatus, pts;
+  void release() {
+    nkeys = 0;
+    lines.release();
+    kstatus.release();
+    pts.release();
+  }
+};
+
 struct BlsDev {
   int ord = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint32_t nkeys = 0;             // keys in the prepared set (lines of 1 + nkeys points)
-  Buf<uint32_t> lines;
-  Buf<uint8_t> kstatus, pts;
+  KeySet keys;                    // pv_bls_set_keys
+  KeySet multi;                   // per call of pv_bls_verify_multi_batch
   // per-call workspaces
   Buf<uint32_t> msgtab, cnt, seg, cursor, order, total, midx, kidx;
-  Buf<uint8_t> sig, blob, verdict, sks;
-  Buf<uint64_t> off;
+  Buf<uint8_t> sig, blob, verdict, sks, mpks;
+  Buf<uint64_t> off, moff;
   float ms_hash = 0, ms_verify = 0;
 };
 
@@ -266,16 +338,19 @@ struct Guard {
 
 unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-// grouping + verify on device buffers, on d.stream (or s)
-int enqueue_verify(BlsDev& d, const uint8_t* sig, const uint8_t* blob, const uint64_t* off, uint64_t n_msgs,
-                   const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n, uint8_t* verdict, hipStream_t s) {
-  if (!d.nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", d.ord);
-  if (n > 0xffffffffull - 64ull * d.nkeys) return bfail(PV_EINVAL, "too many checks in one call");
-  const uint64_t slots = ((n + 63) / 64 + d.nkeys) * 64;
+// grouping + verify on device buffers against key set `ks`, on stream s.
+// Verdicts of checks the kernels skip (key index out of range) stay 0.
+int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_t* blob, const uint64_t* off,
+                   uint64_t n_msgs, const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n, uint8_t* verdict,
+                   hipStream_t s) {
+  if (!ks.nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", d.ord);
+  if (n > 0xffffffffull - 64ull * ks.nkeys) return bfail(PV_EINVAL, "too many checks in one call");
+  if (n_msgs > 0xffffffffull) return bfail(PV_EINVAL, "too many messages in one call");
+  const uint64_t slots = ((n + 63) / 64 + ks.nkeys) * 64;
   BLS_HIP(d.msgtab.ensure(n_msgs * MSG_WORDS));
-  BLS_HIP(d.cnt.ensure(d.nkeys));
-  BLS_HIP(d.cursor.ensure(d.nkeys));
-  BLS_HIP(d.seg.ensure(d.nkeys));
+  BLS_HIP(d.cnt.ensure(ks.nkeys));
+  BLS_HIP(d.cursor.ensure(ks.nkeys));
+  BLS_HIP(d.seg.ensure(ks.nkeys));
   BLS_HIP(d.total.ensure(1));
   BLS_HIP(d.order.ensure(slots));
   BLS_HIP(hipEventRecord(d.ev[0], s));
@@ -283,19 +358,44 @@ int enqueue_verify(BlsDev& d, const uint8_t* sig, const uint8_t* blob, const uin
                                  d.msgtab.p);
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[1], s));
-  BLS_HIP(hipMemsetAsync(d.cnt.p, 0, d.nkeys * 4, s));
-  BLS_HIP(hipMemsetAsync(d.cursor.p, 0, d.nkeys * 4, s));
+  BLS_HIP(hipMemsetAsync(verdict, 0, n, s));
+  BLS_HIP(hipMemsetAsync(d.cnt.p, 0, ks.nkeys * 4, s));
+  BLS_HIP(hipMemsetAsync(d.cursor.p, 0, ks.nkeys * 4, s));
   BLS_HIP(hipMemsetAsync(d.order.p, 0xff, slots * 4, s));
-  hipLaunchKernelGGL(k_bls_count, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, d.cnt.p);
-  hipLaunchKernelGGL(k_bls_segments, dim3(1), dim3(64), 0, s, d.cnt.p, d.nkeys, d.seg.p, d.total.p);
-  hipLaunchKernelGGL(k_bls_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, d.seg.p, d.cursor.p,
-                     d.order.p);
+  hipLaunchKernelGGL(k_bls_count, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, ks.nkeys, d.cnt.p);
+  hipLaunchKernelGGL(k_bls_segments, dim3(1), dim3(64), 0, s, d.cnt.p, ks.nkeys, d.seg.p, d.total.p);
+  hipLaunchKernelGGL(k_bls_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, ks.nkeys, d.seg.p,
+                     d.cursor.p, d.order.p);
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[2], s));
   hipLaunchKernelGGL(k_bls_verify, dim3(blocks_for(slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx, key_idx,
-                     d.order.p, d.total.p, d.msgtab.p, d.lines.p, d.kstatus.p, verdict);
+                     d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs, verdict);
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[3], s));
+  return PV_OK;
+}
+
+// host-side argument checks of the host-buffer entry points: offsets
+// non-decreasing, message indices in range
+int check_messages(const uint64_t* msg_off, uint64_t n_msgs, const uint32_t* msg_idx, uint64_t n) {
+  for (uint64_t i = 0; i < n_msgs; ++i)
+    if (msg_off[i + 1] < msg_off[i]) return bfail(PV_EINVAL, "msg_off not monotone at %llu", (unsigned long long)i);
+  for (uint64_t j = 0; j < n; ++j)
+    if (msg_idx[j] >= n_msgs) return bfail(PV_EINVAL, "msg_idx[%llu] = %u out of range", (unsigned long long)j, msg_idx[j]);
+  return PV_OK;
+}
+
+// messages to the device workspace (offsets rebased to 0, 64 zero bytes of tail pad)
+int upload_messages(BlsDev& d, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n_msgs, hipStream_t s,
+                    std::vector<uint64_t>& off) {
+  const uint64_t b0 = msg_off[0], bytes = msg_off[n_msgs] - b0;
+  BLS_HIP(d.blob.ensure(bytes + 64));
+  BLS_HIP(d.off.ensure(n_msgs + 1));
+  off.resize(n_msgs + 1);
+  for (uint64_t i = 0; i <= n_msgs; ++i) off[i] = msg_off[i] - b0;
+  if (bytes) BLS_HIP(hipMemcpyAsync(d.blob.p, msg_blob + b0, bytes, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemsetAsync(d.blob.p + bytes, 0, 64, s));
+  BLS_HIP(hipMemcpyAsync(d.off.p, off.data(), (n_msgs + 1) * 8, hipMemcpyHostToDevice, s));
   return PV_OK;
 }
 
@@ -321,24 +421,25 @@ int pv_bls_set_keys(const uint8_t* gen, const uint8_t* pks, uint64_t k, uint8_t*
   if (k > 65535) return bfail(PV_EINVAL, "at most 65535 keys per set (got %llu)", (unsigned long long)k);
   BlsDev* d = nullptr;
   if (int rc = bls_dev(device, &d)) return rc;
+  // the old set is gone from here on: a failure below leaves NO set (verify ->
+  // PV_ENOTINIT), never a key count over freed or half-written tables
+  d->keys.nkeys = 0;
   BLS_HIP(hipSetDevice(device));
+  KeySet& ks = d->keys;
   const uint64_t np = k + 1;
-  BLS_HIP(d->pts.ensure(np * 128));
-  BLS_HIP(d->lines.ensure(np * KEY_LINE_WORDS));
-  BLS_HIP(d->kstatus.ensure(np));
-  BLS_HIP(hipMemcpyAsync(d->pts.p, gen, 128, hipMemcpyHostToDevice, d->stream));
-  if (k) BLS_HIP(hipMemcpyAsync(d->pts.p + 128, pks, k * 128, hipMemcpyHostToDevice, d->stream));
-  hipLaunchKernelGGL(k_bls_lines, dim3(blocks_for(np, 64)), dim3(64), 0, d->stream, d->pts.p, (uint32_t)np, d->lines.p,
-                     d->kstatus.p);
+  BLS_HIP(ks.pts.ensure(np * 128));
+  BLS_HIP(ks.lines.ensure(np * KEY_LINE_WORDS));
+  BLS_HIP(ks.kstatus.ensure(np));
+  BLS_HIP(hipMemcpyAsync(ks.pts.p, gen, 128, hipMemcpyHostToDevice, d->stream));
+  if (k) BLS_HIP(hipMemcpyAsync(ks.pts.p + 128, pks, k * 128, hipMemcpyHostToDevice, d->stream));
+  hipLaunchKernelGGL(k_bls_lines, dim3(blocks_for(np, 64)), dim3(64), 0, d->stream, ks.pts.p, (uint32_t)np, ks.lines.p,
+                     ks.kstatus.p);
   BLS_HIP(hipGetLastError());
   std::vector<uint8_t> st(np);
-  BLS_HIP(hipMemcpyAsync(st.data(), d->kstatus.p, np, hipMemcpyDeviceToHost, d->stream));
+  BLS_HIP(hipMemcpyAsync(st.data(), ks.kstatus.p, np, hipMemcpyDeviceToHost, d->stream));
   BLS_HIP(hipStreamSynchronize(d->stream));
-  if (st[0] != 0) {
-    d->nkeys = 0;
-    return bfail(PV_EINVAL, "the generator is not a point of order r on the twist (status %d)", st[0]);
-  }
-  d->nkeys = (uint32_t)k;
+  if (st[0] != 0) return bfail(PV_EINVAL, "the generator is not a point of order r on the twist (status %d)", st[0]);
+  ks.nkeys = (uint32_t)k;
   if (status) memcpy(status, st.data() + 1, k);
   return PV_OK;
 }
@@ -354,7 +455,7 @@ int pv_bls_verify_batch_device(const uint8_t* sig, const uint8_t* msg_blob, cons
   if (!sig || !msg_off || !msg_idx || !key_idx || !verdict || (n_msgs && !msg_blob)) return bfail(PV_EINVAL, "null buffer");
   BLS_HIP(hipSetDevice(device));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->stream;
-  if (int rc = enqueue_verify(*d, sig, msg_blob, msg_off, n_msgs, msg_idx, key_idx, n, verdict, s)) return rc;
+  if (int rc = enqueue_verify(*d, d->keys, sig, msg_blob, msg_off, n_msgs, msg_idx, key_idx, n, verdict, s)) return rc;
   BLS_HIP(hipStreamSynchronize(s));
   return collect_times(*d);
 }
@@ -369,32 +470,25 @@ int pv_bls_verify_batch(const uint8_t* sig, const uint64_t* sig_len, const uint8
   if (n == 0) return PV_OK;
   if (!sig || !msg_off || !msg_idx || !key_idx || !verdict || (n_msgs && !msg_blob && msg_off[n_msgs] != msg_off[0]))
     return bfail(PV_EINVAL, "null buffer");
-  if (!d->nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", device);
+  if (!d->keys.nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", device);
   // host-side argument checks: every index in range, offsets non-decreasing
-  for (uint64_t i = 0; i < n_msgs; ++i)
-    if (msg_off[i + 1] < msg_off[i]) return bfail(PV_EINVAL, "msg_off not monotone at %llu", (unsigned long long)i);
-  for (uint64_t j = 0; j < n; ++j) {
-    if (msg_idx[j] >= n_msgs) return bfail(PV_EINVAL, "msg_idx[%llu] = %u out of range", (unsigned long long)j, msg_idx[j]);
-    if (key_idx[j] >= d->nkeys) return bfail(PV_EINVAL, "key_idx[%llu] = %u out of range", (unsigned long long)j, key_idx[j]);
-  }
+  if (int rc = check_messages(msg_off, n_msgs, msg_idx, n)) return rc;
+  for (uint64_t j = 0; j < n; ++j)
+    if (key_idx[j] >= d->keys.nkeys)
+      return bfail(PV_EINVAL, "key_idx[%llu] = %u out of range", (unsigned long long)j, key_idx[j]);
   BLS_HIP(hipSetDevice(device));
-  const uint64_t b0 = msg_off[0], bytes = msg_off[n_msgs] - b0;
   BLS_HIP(d->sig.ensure(n * 128));
-  BLS_HIP(d->blob.ensure(bytes + 64));
-  BLS_HIP(d->off.ensure(n_msgs + 1));
   BLS_HIP(d->midx.ensure(n));
   BLS_HIP(d->kidx.ensure(n));
   BLS_HIP(d->verdict.ensure(n));
-  std::vector<uint64_t> off(n_msgs + 1);
-  for (uint64_t i = 0; i <= n_msgs; ++i) off[i] = msg_off[i] - b0;
   hipStream_t s = d->stream;
+  std::vector<uint64_t> off;
+  if (int rc = upload_messages(*d, msg_blob, msg_off, n_msgs, s, off)) return rc;
   BLS_HIP(hipMemcpyAsync(d->sig.p, sig, n * 128, hipMemcpyHostToDevice, s));
-  if (bytes) BLS_HIP(hipMemcpyAsync(d->blob.p, msg_blob + b0, bytes, hipMemcpyHostToDevice, s));
-  BLS_HIP(hipMemsetAsync(d->blob.p + bytes, 0, 64, s));
-  BLS_HIP(hipMemcpyAsync(d->off.p, off.data(), (n_msgs + 1) * 8, hipMemcpyHostToDevice, s));
   BLS_HIP(hipMemcpyAsync(d->midx.p, msg_idx, n * 4, hipMemcpyHostToDevice, s));
   BLS_HIP(hipMemcpyAsync(d->kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, s));
-  if (int rc = enqueue_verify(*d, d->sig.p, d->blob.p, d->off.p, n_msgs, d->midx.p, d->kidx.p, n, d->verdict.p, s))
+  if (int rc = enqueue_verify(*d, d->keys, d->sig.p, d->blob.p, d->off.p, n_msgs, d->midx.p, d->kidx.p, n,
+                              d->verdict.p, s))
     return rc;
   BLS_HIP(hipMemcpyAsync(verdict, d->verdict.p, n, hipMemcpyDeviceToHost, s));
   BLS_HIP(hipStreamSynchronize(s));
@@ -404,6 +498,98 @@ int pv_bls_verify_batch(const uint8_t* sig, const uint64_t* sig_len, const uint8
     for (uint64_t j = 0; j < n; ++j)
       if (sig_len[j] != 128) verdict[j] = 0;
   return collect_times(*d);
+}
+
+int pv_bls_verify_multi_batch(const uint8_t* gen, const uint8_t* sig, const uint64_t* sig_len, const uint8_t* msg_blob,
+                              const uint64_t* msg_off, uint64_t n_msgs, const uint32_t* msg_idx, const uint8_t* pks,
+                              const uint64_t* pk_off, uint64_t n, uint8_t* verdict, int device) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  if (n == 0) return PV_OK;
+  if (!gen || !sig || !msg_off || !msg_idx || !pk_off || !verdict ||
+      (n_msgs && !msg_blob && msg_off[n_msgs] != msg_off[0]))
+    return bfail(PV_EINVAL, "null buffer");
+  if (n > 65535) return bfail(PV_EINVAL, "at most 65535 multi-signature checks per call (got %llu)", (unsigned long long)n);
+  if (int rc = check_messages(msg_off, n_msgs, msg_idx, n)) return rc;
+  for (uint64_t j = 0; j < n; ++j)
+    if (pk_off[j + 1] < pk_off[j]) return bfail(PV_EINVAL, "pk_off not monotone at %llu", (unsigned long long)j);
+  const uint64_t p0 = pk_off[0], nk = pk_off[n] - p0;
+  if (nk && !pks) return bfail(PV_EINVAL, "null buffer");
+  BLS_HIP(hipSetDevice(device));
+  KeySet& ks = d->multi;
+  ks.nkeys = 0;
+  const uint64_t np = n + 1;
+  BLS_HIP(ks.pts.ensure(np * 128));
+  BLS_HIP(ks.lines.ensure(np * KEY_LINE_WORDS));
+  BLS_HIP(ks.kstatus.ensure(np));
+  BLS_HIP(d->mpks.ensure(nk * 128));
+  BLS_HIP(d->moff.ensure(np));
+  BLS_HIP(d->sig.ensure(n * 128));
+  BLS_HIP(d->midx.ensure(n));
+  BLS_HIP(d->kidx.ensure(n));
+  BLS_HIP(d->verdict.ensure(n));
+  hipStream_t s = d->stream;
+  std::vector<uint64_t> off, poff(np);
+  std::vector<uint32_t> kid(n);
+  for (uint64_t j = 0; j <= n; ++j) poff[j] = pk_off[j] - p0;
+  for (uint64_t j = 0; j < n; ++j) kid[j] = (uint32_t)j;
+  if (int rc = upload_messages(*d, msg_blob, msg_off, n_msgs, s, off)) return rc;
+  BLS_HIP(hipMemcpyAsync(ks.pts.p, gen, 128, hipMemcpyHostToDevice, s));
+  if (nk) BLS_HIP(hipMemcpyAsync(d->mpks.p, pks + 128 * p0, nk * 128, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemcpyAsync(d->moff.p, poff.data(), np * 8, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemcpyAsync(d->sig.p, sig, n * 128, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemcpyAsync(d->midx.p, msg_idx, n * 4, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemcpyAsync(d->kidx.p, kid.data(), n * 4, hipMemcpyHostToDevice, s));
+  // the aggregated key of every check, then its lines (point 0: the generator)
+  hipLaunchKernelGGL(k_bls_agg_g2, dim3(blocks_for(n, 64)), dim3(64), 0, s, d->mpks.p, d->moff.p, (uint32_t)n, ks.pts.p);
+  hipLaunchKernelGGL(k_bls_lines, dim3(blocks_for(np, 64)), dim3(64), 0, s, ks.pts.p, (uint32_t)np, ks.lines.p,
+                     ks.kstatus.p);
+  BLS_HIP(hipGetLastError());
+  ks.nkeys = (uint32_t)n;
+  if (int rc = enqueue_verify(*d, ks, d->sig.p, d->blob.p, d->off.p, n_msgs, d->midx.p, d->kidx.p, n, d->verdict.p, s))
+    return rc;
+  uint8_t gst = 0xff;
+  BLS_HIP(hipMemcpyAsync(verdict, d->verdict.p, n, hipMemcpyDeviceToHost, s));
+  BLS_HIP(hipMemcpyAsync(&gst, ks.kstatus.p, 1, hipMemcpyDeviceToHost, s));
+  BLS_HIP(hipStreamSynchronize(s));
+  if (gst != 0) {
+    memset(verdict, 0, n);
+    return bfail(PV_EINVAL, "the generator is not a point of order r on the twist (status %d)", gst);
+  }
+  if (sig_len)
+    for (uint64_t j = 0; j < n; ++j)
+      if (sig_len[j] != 128) verdict[j] = 0;
+  return collect_times(*d);
+}
+
+int pv_bls_aggregate_sigs(const uint8_t* sigs, const uint64_t* set_off, uint64_t m, uint8_t* out, int device) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  if (m == 0) return PV_OK;
+  if (!set_off || !out) return bfail(PV_EINVAL, "null buffer");
+  if (m > 0xffffffffull) return bfail(PV_EINVAL, "too many sets");
+  for (uint64_t j = 0; j < m; ++j)
+    if (set_off[j + 1] < set_off[j]) return bfail(PV_EINVAL, "set_off not monotone at %llu", (unsigned long long)j);
+  const uint64_t s0 = set_off[0], ns = set_off[m] - s0;
+  if (ns && !sigs) return bfail(PV_EINVAL, "null buffer");
+  BLS_HIP(hipSetDevice(device));
+  hipStream_t s = d->stream;
+  std::vector<uint64_t> so(m + 1);
+  for (uint64_t j = 0; j <= m; ++j) so[j] = set_off[j] - s0;
+  BLS_HIP(d->sig.ensure(ns * 128));
+  BLS_HIP(d->moff.ensure(m + 1));
+  BLS_HIP(d->blob.ensure(m * 128));
+  if (ns) BLS_HIP(hipMemcpyAsync(d->sig.p, sigs + 128 * s0, ns * 128, hipMemcpyHostToDevice, s));
+  BLS_HIP(hipMemcpyAsync(d->moff.p, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_bls_agg_g1, dim3(blocks_for(m, 64)), dim3(64), 0, s, d->sig.p, d->moff.p, (uint32_t)m, d->blob.p);
+  BLS_HIP(hipGetLastError());
+  BLS_HIP(hipMemcpyAsync(out, d->blob.p, m * 128, hipMemcpyDeviceToHost, s));
+  BLS_HIP(hipStreamSynchronize(s));
+  return PV_OK;
 }
 
 int pv_bls_sign_batch_device(const uint8_t* sks, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n_msgs,
@@ -507,9 +693,9 @@ void pv_bls_shutdown(void) {
   for (auto& d : g_bls) {
     (void)hipSetDevice(d.ord);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
-    d.lines.release(); d.kstatus.release(); d.pts.release(); d.msgtab.release(); d.cnt.release(); d.seg.release();
+    d.keys.release(); d.multi.release(); d.msgtab.release(); d.cnt.release(); d.seg.release();
     d.cursor.release(); d.order.release(); d.total.release(); d.midx.release(); d.kidx.release(); d.sig.release();
-    d.blob.release(); d.verdict.release(); d.sks.release(); d.off.release();
+    d.blob.release(); d.verdict.release(); d.sks.release(); d.off.release(); d.mpks.release(); d.moff.release();
     for (auto& e : d.ev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
     if (d.stream) (void)hipStreamDestroy(d.stream);

@@ -6,6 +6,7 @@ compute entry point is called, the call raises — loudly — instead of silentl
 verifying on the host.
 """
 import ctypes
+import logging
 import os
 import threading
 
@@ -72,15 +73,11 @@ SIGNATURES = [
      [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int,
       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ('pv_curve_stats', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)]),
-    ('pv_set_curve_mode', ctypes.c_int, [ctypes.c_uint32]),
-    ('pv_set_lat_max', ctypes.c_int, [ctypes.c_uint64]),
-    ('pv_set_lat_kernel', ctypes.c_int, [ctypes.c_uint32]),
-    ('pv_set_lat_keyed_max', ctypes.c_int, [ctypes.c_uint64]),
+    ('pv_get_tuning', ctypes.c_int, [_vp]),
+    ('pv_set_tuning', ctypes.c_int, [_vp]),
     ('pv_keycache_add', ctypes.c_int, [_vp, ctypes.c_uint64]),
     ('pv_keycache_clear', ctypes.c_int, []),
     ('pv_keycache_size', ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
-    ('pv_set_host_fused', ctypes.c_int, [ctypes.c_int]),
-    ('pv_set_host_staging', ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
     ('pv_bls_set_keys', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     ('pv_bls_verify_batch', ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
@@ -90,6 +87,9 @@ SIGNATURES = [
      [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp]),
     ('pv_bls_sign_batch', ctypes.c_int,
      [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    ('pv_bls_verify_multi_batch', ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    ('pv_bls_aggregate_sigs', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     ('pv_bls_pubkeys', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     ('pv_bls_kernel_ms', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     ('pv_bls_last_error', ctypes.c_char_p, []),
@@ -108,31 +108,86 @@ def kernel_timing(device, enable):
                                                        ctypes.byref(k)))
     return h.value, c.value, k.value
 
+class Tuning(ctypes.Structure):
+    """struct pv_tuning (include/plenum_verify.h): the schedule knobs.  pv_init
+    reads no environment; tests and tools set these explicitly."""
+    _fields_ = [('struct_size', ctypes.c_uint32), ('curve_mode', ctypes.c_uint32), ('lat_max', ctypes.c_uint64),
+                ('lat_keyed_max', ctypes.c_uint64), ('small_zc_max', ctypes.c_uint64), ('lat_kernel', ctypes.c_uint32),
+                ('host_fused', ctypes.c_uint32), ('host_staging', ctypes.c_uint32), ('host_chunks', ctypes.c_uint32),
+                ('host_first_pct', ctypes.c_uint32), ('host_copy_threads', ctypes.c_uint32),
+                ('host_ramp', ctypes.c_uint64), ('host_pin_max_mb', ctypes.c_uint32), ('host_trace', ctypes.c_uint32),
+                ('test_dup_devices', ctypes.c_uint32), ('reserved', ctypes.c_uint32)]
+
+
 CURVE_MODES = {0: 'half', 1: 'full', 2: 'grouped'}   # PV_CURVE_HALF / _FULL / _GROUPED
+LAT_KERNELS = {'quad': 0, 'pair': 1}                 # PV_LAT_QUAD / PV_LAT_PAIR
+STAGING_MODES = {0: 'pinned', 1: 'pageable'}         # PV_STAGING_PINNED / _PAGEABLE
+LAT_MAX_DEFAULT = 32768                              # defaults of pv_tuning (csrc/pv_api.cpp)
+LAT_KEYED_MAX_DEFAULT = 8192
+
+
+def get_tuning():
+    """The current pv_tuning as a dict (names of include/plenum_verify.h)."""
+    t = Tuning(struct_size=ctypes.sizeof(Tuning))
+    _check('pv_get_tuning', load().pv_get_tuning(ctypes.byref(t)))
+    return {f: getattr(t, f) for f, _ in Tuning._fields_ if f not in ('struct_size', 'reserved')}
+
+
+def set_tuning(**kw):
+    """Change pv_tuning fields (the others keep their values); validated as a
+    whole by pv_set_tuning, applied to initialised devices and later pv_init.
+    Returns the previous values of the changed fields (to restore them)."""
+    cur = get_tuning()
+    bad = set(kw) - set(cur)
+    if bad:
+        raise KeyError('unknown tuning field(s): {}'.format(sorted(bad)))
+    t = Tuning(struct_size=ctypes.sizeof(Tuning), **{**cur, **kw})
+    _check('pv_set_tuning', load().pv_set_tuning(ctypes.byref(t)))
+    return {k: cur[k] for k in kw}
+
+
+# environment names of the tuning fields, for the A/B tools only (tuning_from_env)
+ENV_TUNING = {'PV_CURVE_MODE': ('curve_mode', {v: k for k, v in CURVE_MODES.items()}.get),
+              'PV_LAT_MAX': ('lat_max', int), 'PV_LAT_KEYED_MAX': ('lat_keyed_max', int),
+              'PV_SMALL_ZC_MAX': ('small_zc_max', int), 'PV_LAT_KERNEL': ('lat_kernel', LAT_KERNELS.get),
+              'PV_HOST_FUSED': ('host_fused', int),
+              'PV_HOST_STAGING': ('host_staging', {v: k for k, v in STAGING_MODES.items()}.get),
+              'PV_HOST_CHUNKS': ('host_chunks', int), 'PV_HOST_FIRST_PCT': ('host_first_pct', int),
+              'PV_HOST_COPY_THREADS': ('host_copy_threads', int), 'PV_HOST_RAMP': ('host_ramp', int),
+              'PV_HOST_PIN_MAX_MB': ('host_pin_max_mb', int), 'PV_HOST_TRACE': ('host_trace', int)}
+
+
+def tuning_from_env(environ=None):
+    """Explicit opt-in for A/B tools and bench experiments: apply the PV_* tuning
+    variables that are set in `environ` (default os.environ).  The library itself
+    never reads the environment.  Returns the fields changed."""
+    environ = os.environ if environ is None else environ
+    kw = {}
+    for var, (field, conv) in ENV_TUNING.items():
+        if var in environ:
+            v = conv(environ[var])
+            if v is None:
+                raise ValueError('{}={!r} is not a valid value'.format(var, environ[var]))
+            kw[field] = v
+    if kw:
+        set_tuning(**kw)
+    return kw
 
 
 def set_curve_mode(name):
-    """Curve-stage schedule of generic batches on every initialised device (pv_set_curve_mode)."""
-    code = {v: k for k, v in CURVE_MODES.items()}[name]
-    _check('pv_set_curve_mode', load().pv_set_curve_mode(code))
-
-
-LAT_MAX_DEFAULT = 32768   # PV_LAT_MAX in csrc/pv_api.cpp
+    """Curve-stage schedule of generic batches ('half', 'full', 'grouped')."""
+    set_tuning(curve_mode={v: k for k, v in CURVE_MODES.items()}[name])
 
 
 def set_lat_max(max_signatures):
     """Largest generic batch that runs the latency-mode curve kernel (8 lanes
-    per signature) on every initialised device; 0 disables (pv_set_lat_max)."""
-    _check('pv_set_lat_max', load().pv_set_lat_max(int(max_signatures)))
-
-
-LAT_KEYED_MAX_DEFAULT = 8192   # PV_LAT_KEYED_MAX in csrc/pv_api.cpp
+    per signature); 0 disables."""
+    set_tuning(lat_max=int(max_signatures))
 
 
 def set_lat_keyed_max(max_signatures):
-    """Largest keyed batch (prepared keys) that runs the keyed latency kernel
-    on every initialised device; 0 disables (pv_set_lat_keyed_max)."""
-    _check('pv_set_lat_keyed_max', load().pv_set_lat_keyed_max(int(max_signatures)))
+    """Largest keyed batch (prepared keys) that runs the keyed latency kernel; 0 disables."""
+    set_tuning(lat_keyed_max=int(max_signatures))
 
 
 def keycache_add(keys):
@@ -155,18 +210,43 @@ _pending_keys = []   # keys registered before / between GPU calls (keycache_defe
 def keycache_defer(raw):
     """Queue a 32-byte key for the device key cache; it is added by the next
     host-buffer verify call (no GPU work here: addIdr may run before pv_init)."""
+    global _cache_dropped
     raw = bytes(raw)
     if len(raw) == 32:
         with _lock:
+            if _cached_estimate() + len(_pending_keys) >= KEYCACHE_MAX:
+                _cache_dropped += 1          # over the cap: verified uncached
+                return
             _pending_keys.append(raw)
 
 
+def _cached_estimate():
+    """keys already in the device cache (0 before the engine is initialised)"""
+    if _inited_mask is None or _lib is None:
+        return 0
+    c = ctypes.c_uint64()
+    return c.value if _lib.pv_keycache_size(ctypes.byref(c)) == 0 else 0
+
+
+KEYCACHE_MAX = 1 << 18   # keys queued for the device cache at most (9,344 B each on every device)
+_cache_dropped = 0
+
+
 def _flush_keycache():
+    """Add the queued keys to the device cache.  Best effort: the cache only
+    speeds verification up (uncached keys take the generic kernels), so a
+    failure here (e.g. the cache cannot grow) is counted and the keys are
+    dropped, never raised into the verify call that triggered the flush."""
+    global _cache_dropped
     if _pending_keys:
         with _lock:
             keys = list(_pending_keys)
             _pending_keys.clear()
-        keycache_add(keys)
+        try:
+            keycache_add(keys)
+        except PlenumGpuError as e:
+            _cache_dropped += len(keys)
+            logging.getLogger(__name__).warning('device key cache: %d keys not cached (%s)', len(keys), e)
 
 
 def keycache_clear():
@@ -182,28 +262,26 @@ def keycache_size():
     return c.value
 
 
-LAT_KERNELS = {'quad': 0, 'pair': 1}   # PV_LAT_QUAD / PV_LAT_PAIR
-
-
 def set_lat_kernel(name):
-    """Latency kernel on every initialised device: 'quad' (default, lane quads
-    per point) or 'pair' (the lane-pair kernel, A/B) (pv_set_lat_kernel)."""
-    _check('pv_set_lat_kernel', load().pv_set_lat_kernel(LAT_KERNELS[name]))
+    """Latency kernel: 'quad' (default, lane quads per point) or 'pair' (A/B)."""
+    set_tuning(lat_kernel=LAT_KERNELS[name])
 
 
 def set_host_fused(enable):
     """Host-buffer chunks: one fused launch per chunk + a deferred pass (True,
-    default) or the hash / lattice / curve launches per chunk (pv_set_host_fused)."""
-    _check('pv_set_host_fused', load().pv_set_host_fused(1 if enable else 0))
-
-
-STAGING_MODES = {0: 'pinned', 1: 'pageable'}   # PV_STAGING_PINNED / _PAGEABLE
+    default) or the hash / lattice / curve launches per chunk."""
+    set_tuning(host_fused=1 if enable else 0)
 
 
 def set_host_staging(name, copy_threads=0, chunks=0):
-    """Host-buffer staging of pv_verify_batch on every initialised device (pv_set_host_staging)."""
-    code = {v: k for k, v in STAGING_MODES.items()}[name]
-    _check('pv_set_host_staging', load().pv_set_host_staging(code, int(copy_threads), int(chunks)))
+    """Host-buffer staging of pv_verify_batch ('pinned' / 'pageable'); copy_threads
+    / chunks 0 keep the current values."""
+    kw = {'host_staging': {v: k for k, v in STAGING_MODES.items()}[name]}
+    if copy_threads:
+        kw['host_copy_threads'] = int(copy_threads)
+    if chunks:
+        kw['host_chunks'] = int(chunks)
+    set_tuning(**kw)
 
 
 def curve_stats(device=0):
@@ -439,6 +517,52 @@ def bls_verify_arrays(sig, blob, off, msg_idx, key_idx, sig_len=None, device=0):
             _ptr(sig), _ptr(sl) if sl is not None else None, _ptr(blob), _ptr(off), off.shape[0] - 1, _ptr(msg_idx),
             _ptr(key_idx), n, _ptr(verdict), device))
     return verdict.astype(bool)
+
+
+def bls_verify_multi_arrays(gen, sig, blob, off, msg_idx, pks, pk_off, sig_len=None, device=0):
+    """pv_bls_verify_multi_batch: check j = (sig j (n,128) u8, message msg_idx[j] of
+    (blob, off), the sum of keys pks[pk_off[j]:pk_off[j+1]] ((k,128) u8)) against
+    the generator `gen` -> verdict (n,) bool.  The key set of bls_set_keys is kept."""
+    ensure_init()
+    gen = np.ascontiguousarray(np.frombuffer(bytes(gen), np.uint8))
+    if gen.size != 128:
+        raise ValueError('the generator representation is 128 bytes')
+    sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 128)
+    n = sig.shape[0]
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    msg_idx = np.ascontiguousarray(msg_idx, dtype=np.uint32)
+    pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(-1, 128)
+    pk_off = np.ascontiguousarray(pk_off, dtype=np.uint64)
+    if msg_idx.shape != (n,) or pk_off.shape != (n + 1,):
+        raise ValueError('msg_idx needs n entries and pk_off n + 1')
+    if n and int(pk_off[-1]) > pks.shape[0]:
+        raise ValueError('pk_off exceeds the key array')
+    sl = None if sig_len is None else np.ascontiguousarray(sig_len, dtype=np.uint64)
+    if sl is not None and sl.shape != (n,):
+        raise ValueError('sig_len must have one entry per signature')
+    verdict = np.zeros(n, np.uint8)
+    if n:
+        _bls_check('pv_bls_verify_multi_batch', load().pv_bls_verify_multi_batch(
+            _ptr(gen), _ptr(sig), _ptr(sl) if sl is not None else None, _ptr(blob), _ptr(off), off.shape[0] - 1,
+            _ptr(msg_idx), _ptr(pks), _ptr(pk_off), n, _ptr(verdict), device))
+    return verdict.astype(bool)
+
+
+def bls_aggregate_sigs(sigs, set_off, device=0):
+    """pv_bls_aggregate_sigs: the G1 sum of sigs[set_off[j]:set_off[j+1]] ((k,128) u8)
+    for every set j -> (m, 128) u8 representations (MultiSignature.new)."""
+    ensure_init()
+    sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(-1, 128)
+    set_off = np.ascontiguousarray(set_off, dtype=np.uint64)
+    m = set_off.shape[0] - 1
+    if m > 0 and int(set_off[-1]) > sigs.shape[0]:
+        raise ValueError('set_off exceeds the signature array')
+    out = np.zeros((max(m, 0), 128), np.uint8)
+    if m > 0:
+        _bls_check('pv_bls_aggregate_sigs', load().pv_bls_aggregate_sigs(_ptr(sigs), _ptr(set_off), m, _ptr(out),
+                                                                          device))
+    return out
 
 
 def bls_sign_arrays(sks, blob, off, msg_idx, key_idx, device=0):

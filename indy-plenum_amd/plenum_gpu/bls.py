@@ -95,6 +95,16 @@ class MultiSignature(Signature):
     pass
 
 
+class ProofOfPossession(BlsEntity):
+    """A G1 point (ursa ProofOfPossession.from_bytes: 128 bytes or IndyCryptoError)."""
+
+    @classmethod
+    def from_bytes(cls, b):
+        if len(b) != REPR_SIZE:
+            raise IndyCryptoError('Invalid len of bytes representation for PointG1')
+        return cls(b)
+
+
 class IndyCryptoBlsUtils:
     """crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:23-66"""
     SEED_LEN = 32
@@ -163,10 +173,17 @@ class MultiSignatureValue:
 
 
 class BlsCryptoVerifierGpu:
-    """BlsCryptoVerifierIndyCrypto (bls_crypto_indy_crypto.py:69-106) with a batch
-    entry point.  Keys are prepared on the device the first time they are seen
-    (pv_bls_set_keys: the generator + every key so far; a pool's node keys are
-    prepared once)."""
+    """BlsCryptoVerifierIndyCrypto (bls_crypto_indy_crypto.py:68-109): the four
+    methods of the reference verifier with the same signatures and None rules,
+    plus batch entry points.  Keys are prepared on the device the first time
+    they are seen (pv_bls_set_keys: the generator + every key so far; a pool's
+    node keys are prepared once).
+
+    Prefetch seam (CommitIngress, plenum_gpu/commit_ingress.py): `prefetch`
+    verifies many (signature, message, key) triples in one GPU pass and keeps
+    the verdicts; `verify_sig` answers from them, so the reference's unchanged
+    per-COMMIT `_validate_signature` -> `verify_sig` makes no GPU call for a
+    prefetched COMMIT.  `drop_prefetched` ends the pass."""
 
     def __init__(self, params: GroupParams, device: int = 0):
         self._generator = IndyCryptoBlsUtils.bls_from_str(params.g, Generator)
@@ -175,6 +192,8 @@ class BlsCryptoVerifierGpu:
         self._device = device
         self._keys = {}          # pk bytes -> index in the device key set
         self._status = []
+        self._prefetched = {}    # (signature str, message bytes, pk bytes) -> verdict
+        self.gpu_calls = 0       # native verify calls made (tests of the prefetch seam)
 
     # -- key set
     def _key_indices(self, pks):
@@ -192,39 +211,135 @@ class BlsCryptoVerifierGpu:
         """PV_BLS_KEY_OK / _INFINITY / _NOT_IN_G2 of a key (prepares it)"""
         return int(self._status[self._key_indices([pk.as_bytes()])[0]])
 
-    # -- checks
+    # -- single-key checks
+    def _verify_raw(self, rows) -> np.ndarray:
+        """rows: [(signature bytes, message bytes, pk bytes)] -> bool array (one GPU pass)"""
+        n = len(rows)
+        if not n:
+            return np.zeros(0, bool)
+        sigs, sig_len, msgs, midx = [], [], {}, []
+        for b, message, _pk in rows:
+            sig_len.append(len(b))
+            sigs.append(b[:REPR_SIZE].ljust(REPR_SIZE, b'\0'))
+            midx.append(msgs.setdefault(bytes(message), len(msgs)))
+        kidx = np.array(self._key_indices([r[2] for r in rows]), np.uint32)
+        blob, off = _native.pack_messages(list(msgs))
+        self.gpu_calls += 1
+        return _native.bls_verify_arrays(np.frombuffer(b''.join(sigs), np.uint8), blob, off,
+                                         np.array(midx, np.uint32), kidx, sig_len=np.array(sig_len, np.uint64),
+                                         device=self._device)
+
     def verify_sig_batch(self, items) -> np.ndarray:
         """items: [(signature: str, message: bytes, bls_pk: VerKey | None)] ->
         bool array, entry i == verify_sig(*items[i])."""
-        n = len(items)
-        out = np.zeros(n, bool)
-        rows, sigs, sig_len, msgs, pks = [], [], [], {}, []
+        out = np.zeros(len(items), bool)
+        rows, where = [], []
         for i, (signature, message, bls_pk) in enumerate(items):
             s = IndyCryptoBlsUtils.bls_from_str(signature, Signature)
             if s is None or bls_pk is None:
                 continue
-            b = s.as_bytes()
-            rows.append(i)
-            sig_len.append(len(b))
-            sigs.append(b[:REPR_SIZE].ljust(REPR_SIZE, b'\0'))
-            msgs.setdefault(bytes(message), len(msgs))
-            pks.append(bls_pk.as_bytes())
-        if not rows:
-            return out
-        kidx = np.array(self._key_indices(pks), np.uint32)
-        midx = np.array([msgs[bytes(items[i][1])] for i in rows], np.uint32)
-        blob, off = _native.pack_messages(list(msgs))
-        got = _native.bls_verify_arrays(np.frombuffer(b''.join(sigs), np.uint8), blob, off, midx, kidx,
-                                        sig_len=np.array(sig_len, np.uint64), device=self._device)
-        out[np.array(rows)] = got
+            rows.append((s.as_bytes(), message, bls_pk.as_bytes()))
+            where.append(i)
+        if rows:
+            out[np.array(where)] = self._verify_raw(rows)
         return out
 
     def verify_sig(self, signature: str, message: bytes, bls_pk: Optional[VerKey]) -> bool:
+        """bls_crypto_indy_crypto.py:73-82"""
+        if self._prefetched and bls_pk is not None:
+            hit = self._prefetched.get((signature, bytes(message), bls_pk.as_bytes()))
+            if hit is not None:
+                return hit
         return bool(self.verify_sig_batch([(signature, message, bls_pk)])[0])
 
+    # -- the prefetch seam (COMMITs of one Looper pass)
+    def prefetch(self, items) -> int:
+        """Verify [(signature str, message bytes, bls_pk VerKey | None)] in one GPU
+        pass and keep the verdicts for verify_sig; returns the number verified."""
+        todo = {}
+        for signature, message, bls_pk in items:
+            if bls_pk is None or not isinstance(signature, str):
+                continue
+            k = (signature, bytes(message), bls_pk.as_bytes())
+            if k not in self._prefetched:
+                todo.setdefault(k, (signature, k[1], bls_pk))
+        if todo:
+            got = self.verify_sig_batch(list(todo.values()))
+            for k, v in zip(todo, got):
+                self._prefetched[k] = bool(v)
+        return len(todo)
+
+    def drop_prefetched(self):
+        self._prefetched.clear()
+
+    # -- multi-signatures (PRE-PREPARE path, ordering)
+    def verify_multi_sig_batch(self, items) -> np.ndarray:
+        """items: [(signature: str, message: bytes, pks: Sequence[VerKey | None])] ->
+        bool array, entry i == verify_multi_sig(*items[i]); ONE GPU pass (the
+        keys of every check summed on the device, lines of each sum, the checks)."""
+        out = np.zeros(len(items), bool)
+        sigs, sig_len, msgs, midx, keys, pk_off, where = [], [], {}, [], [], [0], []
+        for i, (signature, message, pks) in enumerate(items):
+            if None in pks:                  # :86-88
+                continue
+            ms = IndyCryptoBlsUtils.bls_from_str(signature, MultiSignature)
+            if ms is None:                   # :90-93
+                continue
+            b = ms.as_bytes()
+            sig_len.append(len(b))
+            sigs.append(b[:REPR_SIZE].ljust(REPR_SIZE, b'\0'))
+            midx.append(msgs.setdefault(bytes(message), len(msgs)))
+            for pk in pks:
+                kb = pk.as_bytes()
+                keys.append(kb[:REPR_SIZE].ljust(REPR_SIZE, b'\0'))
+            pk_off.append(len(keys))
+            where.append(i)
+        if where:
+            blob, off = _native.pack_messages(list(msgs))
+            self.gpu_calls += 1
+            got = _native.bls_verify_multi_arrays(
+                self._generator.as_bytes(), np.frombuffer(b''.join(sigs), np.uint8), blob, off,
+                np.array(midx, np.uint32), np.frombuffer(b''.join(keys), np.uint8), np.array(pk_off, np.uint64),
+                sig_len=np.array(sig_len, np.uint64), device=self._device)
+            out[np.array(where)] = got
+        return out
+
     def verify_multi_sig(self, signature: str, message: bytes, pks: Sequence[Optional[VerKey]]) -> bool:
-        raise NotImplementedError('multi-signature verification (PRE-PREPARE path) is not on the GPU path; '
-                                  'see DESIGN.md §9')
+        """bls_crypto_indy_crypto.py:84-97: e(sigma, g) == e(H(m), sum of pks)"""
+        return bool(self.verify_multi_sig_batch([(signature, message, pks)])[0])
+
+    def create_multi_sig_batch(self, sets) -> list:
+        """sets: [Sequence[signature str]] -> [multi-signature str], entry j ==
+        create_multi_sig(sets[j]); one GPU launch sums every set."""
+        raw, set_off = [], [0]
+        for signatures in sets:
+            for s in signatures:
+                sig = IndyCryptoBlsUtils.bls_from_str(s, Signature)
+                if sig is None or len(sig.as_bytes()) != REPR_SIZE:
+                    # ursa: bls_from_str -> None, then MultiSignature.new reads None.c_instance
+                    raise AttributeError("'NoneType' object has no attribute 'c_instance'")
+                raw.append(sig.as_bytes())
+            set_off.append(len(raw))
+        if not sets:
+            return []
+        sigs = np.frombuffer(b''.join(raw), np.uint8) if raw else np.zeros(0, np.uint8)
+        out = _native.bls_aggregate_sigs(sigs, np.array(set_off, np.uint64), device=self._device)
+        return [IndyCryptoBlsUtils.bls_to_str(MultiSignature(row.tobytes())) for row in out]
+
+    def create_multi_sig(self, signatures: Sequence[str]) -> str:
+        """bls_crypto_indy_crypto.py:99-102: MultiSignature.new = the sum of the G1 points"""
+        return self.create_multi_sig_batch([signatures])[0]
+
+    def verify_key_proof_of_possession(self, key_proof: Optional[ProofOfPossession],
+                                       bls_pk: Optional[VerKey]) -> bool:
+        """bls_crypto_indy_crypto.py:104-109 -> ursa Bls.verify_pop:
+        e(pop, g) == e(H(pk bytes), pk), H = PointG1::from_hash(SHA-256(ver_key.as_bytes()))
+        with as_bytes() the key's 128-byte representation as given (ursa keeps it).
+        PARITY UNPINNED like every BLS verdict here."""
+        if key_proof is None or bls_pk is None:
+            return False
+        pk = bls_pk.as_bytes()
+        return bool(self._verify_raw([(key_proof.as_bytes(), pk, pk)])[0])
 
     # -- COMMITs
     def validate_commit_batch(self, commits) -> list:
@@ -263,5 +378,5 @@ def commit_quorums(verdicts, senders, batch_off, n_nodes, quorum):
 
 
 __all__ = ['GroupParams', 'GENERATOR', 'BlsGroupParamsLoaderIndyCrypto', 'IndyCryptoError', 'BlsEntity', 'VerKey',
-           'Generator', 'Signature', 'MultiSignature', 'IndyCryptoBlsUtils', 'MultiSignatureValue',
+           'Generator', 'Signature', 'MultiSignature', 'ProofOfPossession', 'IndyCryptoBlsUtils', 'MultiSignatureValue',
            'BlsCryptoVerifierGpu', 'CM_BLS_SIG_WRONG', 'PPR_BLS_MULTISIG_WRONG', 'commit_quorums']

@@ -767,6 +767,58 @@ int bls_oracle_g2_in_subgroup(const uint8_t b[128]) {
   return t.inf;
 }
 
+/* ursa Bls::verify_multi_sig (crypto/bls/indy_crypto/bls_crypto_indy_crypto.py:84-97):
+ * e(sigma, g) == e(H(msg), pk_0 + ... + pk_{k-1}), the keys decoded as keys are
+ * (off the twist = O) and summed from O. */
+int bls_oracle_verify_multi(const uint8_t *sig, uint64_t sig_len, const uint8_t *msg, uint64_t mlen,
+                            const uint8_t *pks, uint64_t k, const uint8_t gen[128]) {
+  init();
+  g1 s, h;
+  g2 g, agg, q;
+  if (!g1_decode(&s, sig, sig_len)) return 0;
+  g2_decode(&g, gen);
+  agg.inf = 1;
+  for (uint64_t t = 0; t < k; ++t) {
+    g2_decode(&q, pks + 128 * t);
+    g2_add(&agg, &agg, &q, 0);
+  }
+  hash_to_g1(&h, msg, mlen);
+  fp12 e1, e2;
+  pairing(&e1, &s, &g);
+  pairing(&e2, &h, &agg);
+  return f12_eq(&e1, &e2);
+}
+
+/* 128-byte representation of the sum of k G2 keys (O: 128 zero bytes) */
+void bls_oracle_aggregate_keys(const uint8_t *pks, uint64_t k, uint8_t out[128]) {
+  init();
+  g2 agg, q;
+  agg.inf = 1;
+  for (uint64_t t = 0; t < k; ++t) {
+    g2_decode(&q, pks + 128 * t);
+    g2_add(&agg, &agg, &q, 0);
+  }
+  g2_encode(out, &agg);
+}
+
+/* ursa MultiSignature::new (:99-102): the sum of k signatures' G1 points (each
+ * decoded as sigma is: 128 bytes, O when it does not decode), as ECP::tobytes
+ * writes it: 0x04|x|y, and O as 0x04|0|1 (AMCL's affine (0, 1) of infinity). */
+void bls_oracle_aggregate_sigs(const uint8_t *sigs, uint64_t k, uint8_t out[128]) {
+  init();
+  g1 agg, s;
+  agg.inf = 1;
+  for (uint64_t t = 0; t < k; ++t) {
+    g1_decode(&s, sigs + 128 * t, 128);
+    g1_add(&agg, &agg, &s);
+  }
+  g1_encode(out, &agg);
+  if (agg.inf) {
+    out[0] = 4;
+    out[64] = 1;
+  }
+}
+
 /* batch: check j = (sig j, message msg_idx[j] of blob/off, key key_idx[j] of keys), threads workers */
 typedef struct {
   const uint8_t *sigs, *blob, *keys, *gen;

@@ -96,3 +96,36 @@ def test_no_cpu_fallback_in_product_package():
             assert 'oracle' not in src.lower().replace('libsodium', ''), fn
             assert 'hostcheck' not in src, fn
             assert 'libsodium.so' not in src, fn
+
+
+def test_library_reads_no_environment(native):
+    """pv_init reads no environment: the library imports no
+    getenv, and the schedule knobs are one explicit pv_tuning struct whose
+    defaults, validation and round trip are checked here (no GPU needed)."""
+    out = subprocess.run(['nm', '-D', '--undefined-only', native.LIB_PATH], capture_output=True, text=True).stdout
+    assert not re.search(r'\bgetenv\b|secure_getenv', out)
+    d = native.get_tuning()
+    assert d == {'curve_mode': 0, 'lat_max': 32768, 'lat_keyed_max': 8192, 'small_zc_max': 2048, 'lat_kernel': 0,
+                 'host_fused': 1, 'host_staging': 0, 'host_chunks': 8, 'host_first_pct': 50, 'host_copy_threads': 8,
+                 'host_ramp': 32768, 'host_pin_max_mb': 512, 'host_trace': 0, 'test_dup_devices': 0}
+    os.environ['PV_CURVE_MODE'] = 'full'        # ignored by the library itself
+    try:
+        assert native.get_tuning()['curve_mode'] == 0
+        for bad in ({'curve_mode': 3}, {'host_chunks': 0}, {'host_ramp': 5}, {'test_dup_devices': 1},
+                    {'host_pin_max_mb': 8}, {'lat_max': (1 << 20) + 1}):
+            with pytest.raises(native.PlenumGpuError):
+                native.set_tuning(**bad)
+            assert native.get_tuning() == d
+        prev = native.set_tuning(curve_mode=2, lat_max=0, host_trace=1)
+        assert native.get_tuning() == dict(d, curve_mode=2, lat_max=0, host_trace=1)
+        native.set_tuning(**prev)
+        assert native.get_tuning() == d
+        assert native.tuning_from_env({'PV_CURVE_MODE': 'grouped', 'PV_HOST_CHUNKS': '4'}) == \
+            {'curve_mode': 2, 'host_chunks': 4}
+        native.set_tuning(curve_mode=0, host_chunks=8)
+        with pytest.raises(ValueError):
+            native.tuning_from_env({'PV_CURVE_MODE': 'fast'})
+        t = native.Tuning(struct_size=ctypes.sizeof(native.Tuning) - 4)
+        assert native.load().pv_get_tuning(ctypes.byref(t)) == -22
+    finally:
+        del os.environ['PV_CURVE_MODE']

@@ -89,6 +89,41 @@ def test_key_status_outside_g2(fx, nat):
         bad = bytearray(gb)
         bad[3] ^= 1
         nat.bls_set_keys(bytes(bad), np.zeros((0, 128), np.uint8))
+    # a failed pv_bls_set_keys leaves NO key set: verify -> PV_ENOTINIT
+    with pytest.raises(nat.PlenumGpuError) as e:
+        nat.bls_verify_arrays(np.zeros((1, 128), np.uint8), *_pack([b'm']), np.zeros(1, np.uint32),
+                              np.zeros(1, np.uint32))
+    assert e.value.code == -77
+
+
+def test_device_entry_out_of_range_indices(fx, nat):
+    """pv_bls_verify_batch_device does not check indices on the host: a check with
+    key_idx >= the key count or msg_idx >= n_msgs gets verdict 0 and touches
+    nothing out of range; the in-range checks of the same call are unaffected."""
+    import torch
+    from plenum_gpu.device import _p, _stream
+    gb = bytes.fromhex(fx['generator_hex'])
+    nk = len(fx['keys'])
+    st = nat.bls_set_keys(gb, np.frombuffer(b''.join(bytes.fromhex(k['pk']) for k in fx['keys']), np.uint8))
+    assert not st.any()
+    good = [c for c in fx['cases'] if c.get('verdict') and 'key' in c and len(c['sig']) == 256][:2]
+    assert len(good) == 2
+    msgs = [bytes.fromhex(c['msg']) for c in good]
+    blob_h, off_h = _pack(msgs)
+    dev = torch.device('cuda', 0)
+    sig = torch.from_numpy(np.stack([np.frombuffer(bytes.fromhex(c['sig']), np.uint8) for c in good] * 3)).to(dev)
+    blob = torch.zeros(blob_h.size + 64, dtype=torch.uint8, device=dev)
+    blob[:blob_h.size] = torch.from_numpy(blob_h.copy()).to(dev)
+    off = torch.from_numpy(off_h.astype(np.int64)).to(dev)
+    kid = [good[0]['key'], good[1]['key'], nk + 5, 0xffffffff, good[0]['key'], good[1]['key']]
+    mid = [0, 1, 0, 1, 7, 0xffffffff]
+    kidx = torch.tensor(np.array(kid, np.uint32).view(np.int32), device=dev)
+    midx = torch.tensor(np.array(mid, np.uint32).view(np.int32), device=dev)
+    verdict = torch.full((6,), 9, dtype=torch.uint8, device=dev)
+    lib = nat.load()
+    nat._bls_check('pv_bls_verify_batch_device', lib.pv_bls_verify_batch_device(
+        _p(sig), _p(blob), _p(off), 2, _p(midx), _p(kidx), 6, _p(verdict), 0, _stream(dev)))
+    assert verdict.cpu().tolist() == [1, 1, 0, 0, 0, 0]
 
 
 def test_10k_checks_vs_oracle(fx, nat, orc):

@@ -68,7 +68,7 @@ def test_c2_full_size_properties(torch_dev):
 def test_curve_modes_identical(torch_dev, raw_vectors, adversarial):
     """The half-size path (default; throughput kernel and both latency-mode
     kernels: lane quads and lane pairs), every record through its full-length
-    form (PV_CURVE_MODE=full: the throughput kernel's full-length tasks and the
+    form (curve_mode PV_CURVE_FULL: the throughput kernel's full-length tasks and the
     quad kernel's deferred form) and the grouped kernel give identical verdicts
     and bitmaps on a 200k C2-shaped batch and on every fixture; the half path's
     deferred records really ran."""

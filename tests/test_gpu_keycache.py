@@ -2,7 +2,7 @@
 cache of host-buffer calls (pv_keycache_add): verdicts must equal the
 libsodium-1.0.18 fixtures whatever mix of cached / uncached keys a call holds,
 and the device keyed path of small batches must equal the synthetic spec and
-the keyed throughput kernel (PV_LAT_KEYED_MAX = 0)."""
+the keyed throughput kernel (tuning.lat_keyed_max = 0)."""
 import numpy as np
 import pytest
 
@@ -85,7 +85,7 @@ def test_keycache_dedup_and_add_idr(nat, raw_vectors):
 
 @pytest.mark.parametrize('n', [1, 8, 100, 1000, 8192])
 def test_keyed_device_latency_kernel(nat, n):
-    """Device keyed batches up to PV_LAT_KEYED_MAX take k_verify_quad_keyed:
+    """Device keyed batches up to tuning.lat_keyed_max take k_verify_quad_keyed:
     verdicts and bitmap equal the synthetic spec (~5 % tampered) and the keyed
     throughput kernel (latency path disabled)."""
     from plenum_gpu.device import SyntheticBatch

@@ -1,5 +1,5 @@
 """The multi-device branch of pv_verify_batch: a fresh child
-process runs with PV_TEST_DUP_DEVICE=2 (two engine devices on GPU 0), so the
+process sets pv_tuning.test_dup_devices = 2 (two engine devices on GPU 0), so the
 per-device worker threads, shard offset rebasing and per-shard error
 aggregation run on a one-GPU box (tests/_multidev_worker.py)."""
 import json
@@ -14,8 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def test_two_engine_devices_shard_and_fail_per_shard():
-    env = dict(os.environ, PV_TEST_DUP_DEVICE='2')
-    p = subprocess.run([sys.executable, '-u', os.path.join(HERE, '_multidev_worker.py')], env=env,
+    p = subprocess.run([sys.executable, '-u', os.path.join(HERE, '_multidev_worker.py')],
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])

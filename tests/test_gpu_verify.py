@@ -218,7 +218,7 @@ def test_host_fused_chunks_and_deferred_pass(nat, raw_vectors, adversarial):
     lattice + half-size curve per task) and the deferred records one
     lane-quad pass over a device-side index list: same verdicts as the
     per-chunk hash / lattice / curve schedule on a 200k C2 batch (~400
-    deferred, several chunks); with PV_CURVE_MODE=full every record is listed,
+    deferred, several chunks); with curve_mode PV_CURVE_FULL every record is listed,
     so the list pass loops over 200k entries with its fixed grid; the
     fixtures (mixed-order, non-canonical, small-order cases) through the
     chunk path (latency path off) match libsodium in both modes."""

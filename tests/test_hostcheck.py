@@ -176,8 +176,10 @@ def test_op_counts_pin_bench_constants(hc):
 
 def test_op_counts_pin_valu_constants(hc):
     """The algorithmic non-MAD work of the roofline's combined figure
-    (bench.W_ADD / W_SUB / W_CARRY_PER_VERIFY, SHA512_BLOCKS_C2), counted on the
-    exact kernel schedule of a half-size verify with a 256-byte message."""
+    (bench.W_ADD / W_SUB / W_CARRY_PER_VERIFY), counted on the exact kernel
+    schedule of a half-size verify with a 256-byte message.  The 3 SHA-512 blocks
+    of R||A||M are counted too but not charged: they run in k_hash, not in the
+    timed curve kernel."""
     import bench
     n = 32
     pk, sig, blob, off = _signed_batch(n, 3)
@@ -187,12 +189,13 @@ def test_op_counts_pin_valu_constants(hc):
     assert abs(int(c[2]) / n - bench.W_ADD_PER_VERIFY) <= 1.0
     assert int(c[6]) == bench.W_SUB_PER_VERIFY * n
     assert abs(int(c[3]) / n - bench.W_CARRY_PER_VERIFY) <= 1.0
-    assert int(c[4]) == bench.SHA512_BLOCKS_C2 * n
+    assert int(c[4]) == 3 * n
+    assert bench.W_HALF_PER_VERIFY == 20 * bench.W_MUL_PER_VERIFY + 16 * bench.W_SQ_PER_VERIFY
     assert bench.W_HALF_PER_VERIFY > 0 and bench.W_FULL_PER_VERIFY > 0
 
 
 def test_op_counts_pin_grouped_constants(hc):
-    """PV_CURVE_MODE=grouped: groups of CURVE_K = 4 signatures share the final inversion."""
+    """curve_mode PV_CURVE_GROUPED: groups of CURVE_K = 4 signatures share the final inversion."""
     import bench
     n = 16
     pk, sig, blob, off = _signed_batch(n, 4)

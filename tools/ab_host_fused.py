@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'
 def main(reps=8, modes=(1, 0)):
     from plenum_gpu import _native as nat
     from plenum_gpu.device import SyntheticBatch
+    nat.tuning_from_env()   # the A/B knobs: explicit opt-in (pv_init reads no env)
     nat.ensure_init()
     b = SyntheticBatch(0, 1 << 20, 256, cfg=2, first=1)
     off = b.off.cpu().numpy().astype(np.uint64)

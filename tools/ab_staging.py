@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'
 def main():
     from plenum_gpu import _native as nat
     from plenum_gpu.device import SyntheticBatch
+    nat.tuning_from_env()   # the A/B knobs: explicit opt-in (pv_init reads no env)
     nat.ensure_init()
     b = SyntheticBatch(0, 1000000, 256, cfg=2)
     pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()

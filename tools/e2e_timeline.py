@@ -19,7 +19,7 @@ def main(d, chunks=9):
             ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0]))
     ev.sort()
     # per-chunk grids: k_curve_half (hash / lattice / curve schedule) or
-    # k_chunk_half (fused chunks, PV_HOST_FUSED=1; no k_hash before them)
+    # k_chunk_half (fused chunks, host_fused 1; no k_hash before them)
     curves = [i for i, e in enumerate(ev) if 'k_curve' in e[2] or 'k_chunk_half' in e[2]]
     first_curve = curves[-chunks]
     prev = curves[-chunks - 1] if len(curves) > chunks else -1

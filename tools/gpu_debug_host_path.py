@@ -7,6 +7,7 @@ sys.path.insert(0, os.path.join(REPO, 'indy-plenum_amd'))
 import numpy as np  # noqa: E402
 from plenum_gpu import _native as nat  # noqa: E402
 
+nat.tuning_from_env()   # the A/B knobs: explicit opt-in (pv_init reads no env)
 nat.ensure_init()
 rng = np.random.default_rng(0)
 for n in (1, 2, 5, 64, 1000):

@@ -17,6 +17,7 @@ SIZES = [int(x) for x in os.environ.get('PV_LAT_SIZES', '1,16,100,256,1000,1024,
 def main():
     from plenum_gpu import _native as nat
     from plenum_gpu.device import SyntheticBatch
+    nat.tuning_from_env()   # the A/B knobs: explicit opt-in (pv_init reads no env)
     nat.ensure_init()
     b = SyntheticBatch(0, max(SIZES), 256, cfg=2, first=99)
     pk, sig = b.pk.cpu().numpy(), b.sig.cpu().numpy()

@@ -1,6 +1,10 @@
 """Per-launch PMC summary of the verify kernels from tools/pmc_passes.sh output.
 
-    python tools/pmc_summary.py gpurun_out/pmc > profiles/rNN_curve_pmc.json
+    python tools/pmc_summary.py gpurun_out/pmc [units] > profiles/rNN_curve_pmc.json
+
+units (optional): the verifies / checks one launch of the dominant kernel
+processed; adds hbm_bytes_per_unit so a bench line can scale the traffic to
+its own launch size.
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reports half the bytes of wide streaming reads, so it is
@@ -17,18 +21,27 @@ import sys
 
 
 def load(d, tag):
-    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    """kernel -> counter -> values over the dispatches of the kernel's LARGEST
+    grid (a bench run also launches the small latency calls; those are not the
+    bench line's launch)"""
+    rows = collections.defaultdict(list)
     for fn in glob.glob(os.path.join(d, tag, '*counter_collection.csv')):
         with open(fn) as fh:
             for r in csv.DictReader(fh):
                 k = r['Kernel_Name'].split('(')[0]
                 if k.startswith('void '):
                     k = k[5:]
-                per[k][r['Counter_Name']].append(float(r['Counter_Value']))
+                rows[k].append((int(r.get('Grid_Size') or 0), r['Counter_Name'], float(r['Counter_Value'])))
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for k, rs in rows.items():
+        g = max(x[0] for x in rs)
+        for grid, c, v in rs:
+            if grid == g:
+                per[k][c].append(v)
     return per
 
 
-def main(d):
+def main(d, units=None):
     out = {'source': d, 'kernels': {}}
     merged = collections.defaultdict(dict)
     for tag in ('fetch', 'write', 'sq1', 'sq2', 'l2'):
@@ -37,7 +50,7 @@ def main(d):
                 # one value per dispatch after summing over XCD/SE instances
                 merged[k][c] = sum(vals) / max(1, len(vals))
     for k, c in merged.items():
-        if not k.startswith('pv::k_'):
+        if not (k.startswith('pv::k_') or k.startswith('pvbls::k_')):
             continue
         e = dict(c)
         if 'FETCH_SIZE' in c and 'WRITE_SIZE' in c:
@@ -54,8 +67,17 @@ def main(d):
     curve_k = next((k for k in names if k.startswith('pv::k_curve') and 'true' not in k), None)
     out['curve_kernel'] = curve_k
     out['hbm_bytes_per_launch'] = out['kernels'].get(curve_k, {}).get('hbm_bytes_per_launch')
+    bls_k = next((k for k in out['kernels'] if k.startswith('pvbls::k_bls_verify')), None)
+    if bls_k:
+        out['check_kernel'] = bls_k
+        if curve_k is None:
+            out['hbm_bytes_per_launch'] = out['kernels'][bls_k].get('hbm_bytes_per_launch')
+    if units:
+        out['units_per_launch'] = units
+        if out['hbm_bytes_per_launch'] is not None:
+            out['hbm_bytes_per_unit'] = out['hbm_bytes_per_launch'] / units
     print(json.dumps(out, indent=1))
 
 
 if __name__ == '__main__':
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
