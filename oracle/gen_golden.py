@@ -36,6 +36,16 @@ Fixtures
                         111-134) with Quorums(n).propagate; a PROPAGATE reaches
                         add_propagate only if ReqAuthenticator.authenticate accepts its
                         request (Node.validateNodeMsg -> verifySignature, node.py:2624-2655)
+  c1_10k.json           BASELINE configs[0] at full size: the 10,000 requests of
+                        plenum_gpu.synth.c1_requests (seed / payload spec of SURVEY.md
+                        8(d)), signed here by the reference DidSigner, with the
+                        mutations tests/test_gpu_c1.py applies (reqId changed after
+                        signing, a non-base58 character, a truncated signature,
+                        identifiers never registered), through the reference
+                        CoreAuthNr(['buy'], [], []).authenticate: every failure's
+                        exception class + text, a digest of the successes, and a
+                        digest of the request dicts (so the GPU-side regeneration is
+                        checked to be the same input)
   ingress.json          one node service pass for the batched-ingestion path (f1):
                         client requests of every shape with the reference
                         Request(**req).key (plenum/common/request.py:82-120) and the
@@ -813,8 +823,57 @@ def gen_merkle():
             'children': [th.hash_children(leaves[i][:32].ljust(32, b'x'), leaves[i + 1][:32].ljust(32, b'y')).hex()
                          for i in range(0, 20, 2)]}
 
+# ------------------------------------------------------- C1 at 10k (configs[0])
+C1_MUTATIONS = {'reqId_plus_1': 'k % 41 == 0', 'bad_base58_first_char': 'k % 173 == 7',
+                'sig_minus_3_chars': 'k % 211 == 11', 'never_registered': 'k % 997 == 5'}
 
-GENERATORS = ['kat', 'plenum_requests', 'raw_vectors', 'adversarial', 'tally', 'ingress', 'merkle', 'propagate']
+
+def c1_mutate(reqs):
+    """tests/test_gpu_c1.py's mutations, in its order"""
+    n = len(reqs)
+    for k in range(0, n, 41):
+        reqs[k]['reqId'] += 1
+    for k in range(7, n, 173):
+        reqs[k]['signature'] = '0' + reqs[k]['signature'][1:]
+    for k in range(11, n, 211):
+        reqs[k]['signature'] = reqs[k]['signature'][:-3]
+    return reqs
+
+
+def c1_digest(obj):
+    return hashlib.sha256(json.dumps(obj, sort_keys=True, separators=(',', ':')).encode()).hexdigest()
+
+
+def gen_c1(n=10_000):
+    sys.path.insert(0, os.path.join(REPO, 'indy-plenum_amd'))
+    from plenum_gpu import synth   # pure seed / payload spec (no GPU)
+    reqs, ids = [], []
+    for j in range(n):
+        sgn = DidSigner(seed=synth.seed(1, j))
+        ids.append((sgn.identifier, sgn.verkey))
+        data = ''.join(chr(97 + b % 26) for b in synth.message(1, j, 256))
+        r = {'identifier': sgn.identifier, 'reqId': j, 'operation': {'type': 'buy', 'data': data},
+             'protocolVersion': 2}
+        r['signature'] = sgn.sign(r)
+        reqs.append(r)
+    c1_mutate(reqs)
+    authnr = CoreAuthNr(['buy'], [], [])
+    for k, (idr, vk) in enumerate(ids):
+        if k % 997 != 5:
+            authnr.addIdr(idr, vk)
+    fails, ok = {}, []
+    for k, r in enumerate(reqs):
+        try:
+            ok.append([k, list(authnr.authenticate(r))])
+        except Exception as ex:  # noqa: BLE001 - the outcome is the fixture
+            fails[str(k)] = [type(ex).__name__, str(ex)]
+    return {'n': n, 'spec': 'plenum_gpu.synth.c1_requests(n) (cfg 1), signed by the reference DidSigner; '
+                            'mutations then CoreAuthNr([\'buy\'], [], []).authenticate',
+            'mutations': C1_MUTATIONS, 'identities_digest': c1_digest(ids), 'requests_digest': c1_digest(reqs),
+            'failures': fails, 'ok_count': len(ok), 'ok_digest': c1_digest(ok)}
+
+
+GENERATORS = ['kat', 'plenum_requests', 'raw_vectors', 'adversarial', 'tally', 'ingress', 'merkle', 'propagate', 'c1']
 
 
 def main(which=None):
@@ -838,6 +897,9 @@ def main(which=None):
     if 'propagate' in which:
         with open(os.path.join(OUT, 'propagate.json'), 'w') as fh:
             json.dump(gen_propagate(), fh, indent=0)
+    if 'c1' in which:
+        with open(os.path.join(OUT, 'c1_10k.json'), 'w') as fh:
+            json.dump(gen_c1(), fh, indent=0, sort_keys=True)
     if 'ingress' in which:
         with open(os.path.join(OUT, 'ingress.json'), 'w') as fh:
             json.dump(gen_ingress(), fh, indent=0)
