@@ -143,17 +143,22 @@ def _traffic_per_launch():
 # by issue class:
 #   fe_mul   9 x 19 g_j (v_mul_u32_u24) + 10 column carries (v_lshrrev_b64) + the
 #            x19 wrap -> 20 half-rate; 5 x 2 f_odd + 10 masks + 2 adds -> 17 full-rate
-#   fe_sq    5 x 19 f + 10 carries + wrap -> 16 half; 9 x 2 f + 10 masks + 2 -> 21 full
-#   fe_add   10 full; fe_sub / fe_neg 20 full (+2p, -g); fe_carry 30 full (shift, mask, add)
+#   fe_sq    5 x 19 f / 38 f + 10 carries + wrap -> 16 half; 8 x 2 f + 10 masks + 2 -> 20 full
+#            (the 13-operand squaring of pv_field.h sq_avail; was 2f_0..9 + 4f_odd)
+#   fe_add   10 full; fe_sub / fe_neg 20 full (+2p, -g); fe_carry 30 full (shift, mask, add);
+#            fe_carry_even 15 full
 # Only work the timed kernel (k_curve_half) does is charged: the SHA-512 of
 # R||A||M runs in k_hash, before it.
-W_ADD_PER_VERIFY, W_SUB_PER_VERIFY, W_CARRY_PER_VERIFY = 723, 778, 164
+W_ADD_PER_VERIFY, W_SUB_PER_VERIFY, W_CARRY_PER_VERIFY = 595, 778, 36
+W_CARRY_EVEN_PER_VERIFY = 128   # the doublings' T: carries out of the even limbs only (fe_carry_even)
+W_SQ2X_PER_VERIFY = 128         # the doublings' 2Z^2 as one squaring (fe_sq2x: 3 more prepared operands)
 HALF_COST = {'mul': 20, 'sq': 16}
-FULL_COST = {'mul': 17, 'sq': 21, 'add': 10, 'sub': 20, 'carry': 30}
+FULL_COST = {'mul': 17, 'sq': 20, 'add': 10, 'sub': 20, 'carry': 30, 'carry_even': 15}
 W_HALF_PER_VERIFY = HALF_COST['mul'] * W_MUL_PER_VERIFY + HALF_COST['sq'] * W_SQ_PER_VERIFY
 W_FULL_PER_VERIFY = (FULL_COST['mul'] * W_MUL_PER_VERIFY + FULL_COST['sq'] * W_SQ_PER_VERIFY
                      + FULL_COST['add'] * W_ADD_PER_VERIFY + FULL_COST['sub'] * W_SUB_PER_VERIFY
-                     + FULL_COST['carry'] * W_CARRY_PER_VERIFY)
+                     + FULL_COST['carry'] * W_CARRY_PER_VERIFY + FULL_COST['carry_even'] * W_CARRY_EVEN_PER_VERIFY
+                     + 3 * W_SQ2X_PER_VERIFY)
 
 
 def _class_rates(peak):

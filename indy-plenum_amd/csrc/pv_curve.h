@@ -30,23 +30,26 @@ PV_HD void ge_p3_0(ge_p3& h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); fe_0(h.T); }
 #ifndef PV_FUSE
 #define PV_FUSE 0
 #endif
+// Operand roles (f = the 2f_odd side, g = the 19g side) are chosen so the
+// prepared operands are shared: T is g of X*T and Z*T (19T once), Z is f of
+// Z*T and Z*Y (2Z_odd once), as X is f of X*T and X*Y in the p3 form.
 PV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
 #if PV_FUSE & 2
-  fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  fe_mul2(r.X, p.X, p.T, r.Y, p.Z, p.Y);
 #else
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
 #endif
   fe_mul(r.Z, p.Z, p.T);
 }
 
 PV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
 #if PV_FUSE & 2
-  fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  fe_mul2(r.X, p.X, p.T, r.Y, p.Z, p.Y);
   fe_mul2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
 #else
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
 #endif
@@ -59,10 +62,11 @@ PV_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
 #if PV_FUSE & 1
   fe_sq2(xx, p.X, yy, p.Y);
   fe_sq2(zz2, p.Z, xy2, t);    // Z^2, (X+Y)^2
+  fe_add(zz2, zz2, zz2);       // 2Z^2
 #else
   fe_sq(xx, p.X);
   fe_sq(yy, p.Y);
-  fe_sq(zz2, p.Z);
+  fe_sq2x(zz2, p.Z);           // 2Z^2 in one squaring (p.Z TIGHT)
   fe_sq(xy2, t);               // (X+Y)^2
 #endif
   fe_add(r.Y, yy, xx);         // LOOSE
@@ -70,9 +74,8 @@ PV_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe_sub4(r.X, xy2, r.Y);      // (X+Y)^2 - X^2 - Y^2 = 2XY, even limbs < 2^28.4:
                                // only ever the FIRST operand of r.X*r.T / r.X*r.Y
                                // (second operand TIGHT / LOOSE), so no carry needed
-  fe_add(t, zz2, zz2);         // 2Z^2, even limbs <= 2^27
-  fe_sub4(r.T, t, r.Z);
-  fe_carry(r.T);
+  fe_sub4(r.T, zz2, r.Z);      // even limbs <= 2^28.4, odd <= 2^27.4
+  fe_carry_even(r.T);          // T is the 19x operand of X*T and Z*T: 19 T_j < 2^32
 }
 
 PV_HD void ge_p3_dbl(ge_p1p1& r, const ge_p3& p) {

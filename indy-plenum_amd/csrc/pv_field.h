@@ -37,6 +37,9 @@
 #ifndef PV_CHECK_SQ
 #define PV_CHECK_SQ(f)
 #endif
+#ifndef PV_CHECK_SQ2X
+#define PV_CHECK_SQ2X(f)
+#endif
 // Optional scheduling fence after every field multiply (-DPV_FE_FENCE_ON):
 // keeps the scheduler from interleaving consecutive multiplies.  Off by
 // default since the column-asm multiply (below): with each column one asm
@@ -281,45 +284,92 @@ PV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   PV_FE_FENCE();
 }
 
-// h = f^2 with the symmetric cross terms folded (55 products instead of 100).
-PV_HD void fe_sq(fe& h, const fe& f) {
-  PV_COUNT(sq);
-  PV_CHECK_SQ(f);
-  uint32_t f2[10], f19[10], f4[10];
+// Squaring operands.  Product (i, j), i <= j, of MULT * f^2 carries the
+// coefficient c = MULT * (i == j ? 1 : 2) * (i, j both odd ? 2 : 1) *
+// (i + j >= 10 ? 19 : 1) and is formed as (m_i f_i)(m_j f_j) with m_i m_j = c
+// from a set of PREPARED multiples, the smallest set that covers all 55
+// products (exhaustive search, tools/sq_prep_search.py):
+//   MULT 1: 13 values  2f_0..7, 19f_6, 19f_8, 38f_5, 38f_7, 38f_9
+//           (against 20 for 2f_0..9, 19f_5..9, 4f_odd); odd limbs <= 2^26.75,
+//           even <= 2^27.75 (LOOSE inputs qualify);
+//   MULT 2: 16 values  2f_0..7, 4f_0, 4f_1, 4f_3, 38f_6, 38f_8, 76f_5, 76f_7,
+//           76f_9 -- 2 f^2 in one squaring (ge_p2_dbl's 2Z^2) instead of a
+//           squaring + 10 adds; TIGHT inputs only (76 f_odd < 2^32).
+// The host build checks every operand and column bound.
+template <int MULT>
+constexpr bool sq_avail(int i, int m) {
+  if (MULT == 1)
+    return m == 1 || (m == 2 && i < 8) || (m == 19 && (i == 6 || i == 8)) || (m == 38 && (i == 5 || i == 7 || i == 9));
+  return m == 1 || (m == 2 && i < 8) || (m == 4 && (i == 0 || i == 1 || i == 3)) || (m == 38 && (i == 6 || i == 8)) ||
+         (m == 76 && (i == 5 || i == 7 || i == 9));
+}
+template <int MULT>
+constexpr int sq_coef(int i, int j) {
+  return MULT * (i == j ? 1 : 2) * ((i & 1) && (j & 1) ? 2 : 1) * (i + j >= 10 ? 19 : 1);
+}
+// the multiple of f_i (first) / f_j (second) used for product (i, j)
+template <int MULT>
+constexpr int sq_pick(int i, int j, bool second) {
+  const int ms[6] = {1, 2, 4, 19, 38, 76};
+  for (int a = 0; a < 6; ++a)
+    for (int b = 0; b < 6; ++b)
+      if (ms[a] * ms[b] == sq_coef<MULT>(i, j) && sq_avail<MULT>(i, ms[a]) && sq_avail<MULT>(j, ms[b]))
+        return second ? ms[b] : ms[a];
+  return 0;
+}
+template <int MULT>
+constexpr bool sq_plan_ok() {
+  for (int i = 0; i < 10; ++i)
+    for (int j = i; j < 10; ++j)
+      if (sq_pick<MULT>(i, j, false) * sq_pick<MULT>(i, j, true) != sq_coef<MULT>(i, j)) return false;
+  return true;
+}
+static_assert(sq_plan_ok<1>() && sq_plan_ok<2>(), "every squaring product needs a prepared operand pair");
+struct sq_ops {
+  uint32_t f[10], f2[10], f4[10], f19[10], f38[10], f76[10];
+};
+PV_HD uint32_t sq_get(const sq_ops& o, int m, int i) {
+  return m == 1 ? o.f[i] : m == 2 ? o.f2[i] : m == 4 ? o.f4[i] : m == 19 ? o.f19[i] : m == 38 ? o.f38[i] : o.f76[i];
+}
+// every multiple of every limb; the ones a plan does not read are dead code
+PV_HD void sq_prepare(sq_ops& o, const fe& f) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) f2[i] = twice(f.v[i]);
+  for (int i = 0; i < 10; ++i) {
+    o.f[i] = f.v[i];
+    o.f2[i] = twice(f.v[i]);
+    o.f4[i] = twice(o.f2[i]);
+    o.f19[i] = 19u * f.v[i];
+    o.f38[i] = 38u * f.v[i];
+    o.f76[i] = 76u * f.v[i];
+  }
+}
+// column k of MULT f^2: (as, bs) with 6 products (k even) or 5 (k odd)
+template <int MULT>
+PV_HD void sq_column(const sq_ops& o, int k, uint32_t as[6], uint32_t bs[6]) {
+  int t = 0;
 #pragma unroll
-  for (int i = 5; i < 10; ++i) f19[i] = 19u * f.v[i];
+  for (int i = 0; i < 10; ++i) {
 #pragma unroll
-  for (int i = 1; i < 10; i += 2) f4[i] = twice(f2[i]);
+    for (int j = i; j < 10; ++j) {
+      if ((i + j) % 10 != k) continue;
+      as[t] = sq_get(o, sq_pick<MULT>(i, j, false), i);
+      bs[t] = sq_get(o, sq_pick<MULT>(i, j, true), j);
+      ++t;
+    }
+  }
+}
+
+// h = MULT f^2 with the symmetric cross terms folded (55 products instead of 100).
+template <int MULT>
+PV_HD void fe_sq_t(fe& h, const fe& f) {
+  sq_ops o;
+  sq_prepare(o, f);
   uint64_t carry = 0;
   uint32_t out[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
     uint32_t as[6], bs[6];
-    int t = 0;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-#pragma unroll
-      for (int j = i; j < 10; ++j) {
-        if ((i + j) % 10 != k) continue;
-        const bool oo = (i & 1) && (j & 1);
-        const bool wrap = i + j >= 10;
-        uint32_t a, b;
-        if (i == j) {
-          // f_i^2 (x2 if odd) (x19 if wrapped)
-          if (!wrap) { a = f.v[i]; b = oo ? f2[i] : f.v[i]; }
-          else { a = oo ? f2[i] : f.v[i]; b = f19[i]; }
-        } else {
-          // 2 f_i f_j (x2 if both odd) (x19 if wrapped)
-          a = oo ? f4[i] : f2[i];
-          b = wrap ? f19[j] : f.v[j];
-        }
-        as[t] = a;
-        bs[t] = b;
-        ++t;
-      }
-    }
+    sq_column<MULT>(o, k, as, bs);
     // column k has 6 products when k is even, 5 when odd
     const uint64_t acc = (k & 1) ? column<5>(as, bs, carry, false) : column<6>(as, bs, carry, k == 0);
     carry = acc >> ((k & 1) ? 25 : 26);
@@ -327,6 +377,17 @@ PV_HD void fe_sq(fe& h, const fe& f) {
   }
   fe_finish_columns(h, carry, out);
   PV_FE_FENCE();
+}
+PV_HD void fe_sq(fe& h, const fe& f) {
+  PV_COUNT(sq);
+  PV_CHECK_SQ(f);
+  fe_sq_t<1>(h, f);
+}
+// h = 2 f^2 (f TIGHT)
+PV_HD void fe_sq2x(fe& h, const fe& f) {
+  PV_COUNT(sq);
+  PV_CHECK_SQ2X(f);
+  fe_sq_t<2>(h, f);
 }
 
 // ---- two / three independent products at once (k_curve_half's hot loop).
@@ -390,16 +451,11 @@ PV_HD void fe_sq_n(fe* const h[C], const fe* const f[C]) {
 #pragma unroll
   for (int c = 0; c < C; ++c) fe_sq(*h[c], *f[c]);
 #else
-  uint32_t f2[C][10], f19[C][10], f4[C][10];
+  sq_ops o[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     PV_COUNT(sq);
-#pragma unroll
-    for (int i = 0; i < 10; ++i) f2[c][i] = twice(f[c]->v[i]);
-#pragma unroll
-    for (int i = 5; i < 10; ++i) f19[c][i] = 19u * f[c]->v[i];
-#pragma unroll
-    for (int i = 1; i < 10; i += 2) f4[c][i] = twice(f2[c][i]);
+    sq_prepare(o[c], *f[c]);
   }
   uint64_t carry[C];
   uint32_t out[C][10];
@@ -407,29 +463,7 @@ PV_HD void fe_sq_n(fe* const h[C], const fe* const f[C]) {
   for (int k = 0; k < 10; ++k) {
     uint32_t as[C][6], bs[C][6];
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      int t = 0;
-#pragma unroll
-      for (int i = 0; i < 10; ++i) {
-#pragma unroll
-        for (int j = i; j < 10; ++j) {
-          if ((i + j) % 10 != k) continue;
-          const bool oo = (i & 1) && (j & 1);
-          const bool wrap = i + j >= 10;
-          uint32_t x, y;
-          if (i == j) {
-            if (!wrap) { x = f[c]->v[i]; y = oo ? f2[c][i] : f[c]->v[i]; }
-            else { x = oo ? f2[c][i] : f[c]->v[i]; y = f19[c][i]; }
-          } else {
-            x = oo ? f4[c][i] : f2[c][i];
-            y = wrap ? f19[c][j] : f[c]->v[j];
-          }
-          as[c][t] = x;
-          bs[c][t] = y;
-          ++t;
-        }
-      }
-    }
+    for (int c = 0; c < C; ++c) sq_column<1>(o[c], k, as[c], bs[c]);
     uint64_t acc[C];
     if constexpr (C == 2) {
       if (k & 1) madc5x2(acc[0], acc[1], as[0], bs[0], as[1], bs[1], carry[0], carry[1]);
@@ -536,6 +570,21 @@ PV_HD void fe_carry(fe& h) {
   c = h.v[7] >> 25; h.v[7] &= M25; h.v[8] += c;
   c = h.v[8] >> 26; h.v[8] &= M26; h.v[9] += c;
   c = h.v[9] >> 25; h.v[9] &= M25; h.v[0] += 19u * c;
+}
+
+// carries out of the EVEN limbs only (into the odd limb above; no wrap):
+// 15 ops instead of 30, five independent chains.  Even limbs -> < 2^26, odd
+// limbs grow by < 2^(max even - 26).  Enough where only the even limbs exceed
+// an operand bound (ge_p2_dbl's T: even <= 2^28.6, odd <= 2^27.6 before,
+// odd <= 2^27.6 + 6 after, so 19 T_j < 2^32 for every j).
+PV_HD void fe_carry_even(fe& h) {
+  PV_COUNT(carry_even);
+#pragma unroll
+  for (int i = 0; i < 10; i += 2) {
+    const uint32_t c = h.v[i] >> 26;
+    h.v[i] &= M26;
+    h.v[i + 1] += c;
+  }
 }
 
 // conditional select: h = c ? g : f  (lane-local, branch-free)

@@ -44,7 +44,7 @@ def hc_verify(hc, pk, sig, blob, off):
 
 
 def counts(hc):
-    c = np.zeros(7, np.uint64)
+    c = np.zeros(8, np.uint64)
     bad = hc.hc_get_counts(_p(c))
     return c, bad
 
@@ -189,6 +189,7 @@ def test_op_counts_pin_valu_constants(hc):
     assert abs(int(c[2]) / n - bench.W_ADD_PER_VERIFY) <= 1.0
     assert int(c[6]) == bench.W_SUB_PER_VERIFY * n
     assert abs(int(c[3]) / n - bench.W_CARRY_PER_VERIFY) <= 1.0
+    assert int(c[7]) == bench.W_CARRY_EVEN_PER_VERIFY * n
     assert int(c[4]) == 3 * n
     assert bench.W_HALF_PER_VERIFY == 20 * bench.W_MUL_PER_VERIFY + 16 * bench.W_SQ_PER_VERIFY
     assert bench.W_HALF_PER_VERIFY > 0 and bench.W_FULL_PER_VERIFY > 0

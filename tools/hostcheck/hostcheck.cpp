@@ -13,7 +13,7 @@
 #include <string.h>
 
 static uint64_t g_cnt[8];
-enum { HC_mul, HC_sq, HC_add, HC_carry, HC_sha, HC_sc, HC_sub };
+enum { HC_mul, HC_sq, HC_add, HC_carry, HC_sha, HC_sc, HC_sub, HC_carry_even };
 static int g_bad_bound = 0;
 
 #define PV_HD static inline
@@ -41,15 +41,42 @@ static void hc_check_mul(const uint32_t* f, const uint32_t* g) {
     if (s >> 64) hc_bad("column", k, (unsigned long long)(s >> 64));
   }
 }
-// fe_sq(f): operands 4 f_odd, 19 f_j and the columns of f*f
+// fe_sq(f): its prepared operands 2 f_0..7, 19 f_6, 19 f_8, 38 f_5, 38 f_7,
+// 38 f_9 (pv_field.h sq_avail) and the columns of f*f
 static void hc_check_sq(const uint32_t* f) {
-  for (int i = 1; i < 10; i += 2)
-    if (4ull * f[i] >= (1ull << 32)) hc_bad("4f", i, f[i]);
-  for (int j = 5; j < 10; ++j)
-    if (38ull * f[j] >= (1ull << 33)) hc_bad("19f", j, f[j]);
+  for (int i = 0; i < 8; ++i)
+    if (2ull * f[i] >= (1ull << 32)) hc_bad("2f", i, f[i]);
+  for (int j = 6; j < 10; j += 2)
+    if (19ull * f[j] >= (1ull << 32)) hc_bad("19f", j, f[j]);
+  for (int j = 5; j < 10; j += 2)
+    if (38ull * f[j] >= (1ull << 32)) hc_bad("38f", j, f[j]);
   hc_check_mul(f, f);
 }
+// fe_sq2x(f) = 2 f^2: 2 f_0..7, 4 f_0,1,3, 38 f_6,8, 76 f_5,7,9 and twice the columns of f*f
+static void hc_check_sq2x(const uint32_t* f) {
+  for (int i = 0; i < 8; ++i)
+    if (2ull * f[i] >= (1ull << 32)) hc_bad("2f", i, f[i]);
+  static const int four[3] = {0, 1, 3};
+  for (int i : four)
+    if (4ull * f[i] >= (1ull << 32)) hc_bad("4f", i, f[i]);
+  for (int j = 6; j < 10; j += 2)
+    if (38ull * f[j] >= (1ull << 32)) hc_bad("38f", j, f[j]);
+  for (int j = 5; j < 10; j += 2)
+    if (76ull * f[j] >= (1ull << 32)) hc_bad("76f", j, f[j]);
+  for (int k = 0; k < 10; ++k) {
+    unsigned __int128 s = (unsigned __int128)1 << 39;
+    for (int i = 0; i < 10; ++i) {
+      const int j = (k - i + 10) % 10;
+      unsigned __int128 t = (unsigned __int128)2 * f[i] * f[j];
+      if ((i & 1) && (j & 1)) t *= 2;
+      if (i + j >= 10) t *= 19;
+      s += t;
+    }
+    if (s >> 64) hc_bad("column2x", k, (unsigned long long)(s >> 64));
+  }
+}
 #define PV_CHECK_MUL(f, g) hc_check_mul((f).v, (g).v)
+#define PV_CHECK_SQ2X(f) hc_check_sq2x((f).v)
 #define PV_CHECK_SQ(f) hc_check_sq((f).v)
 
 #include "../../indy-plenum_amd/csrc/pv_verify_core.h"
@@ -341,9 +368,9 @@ void hc_reset_counts(void) {
   g_bad_bound = 0;
 }
 
-// counts[0..5] = mul, sq, add, carry, sha blocks, scalar reductions
+// counts[0..7] = mul, sq, add, carry, sha blocks, scalar reductions, sub, even-limb carries
 int hc_get_counts(uint64_t* counts) {
-  for (int i = 0; i < 7; ++i) counts[i] = g_cnt[i];
+  for (int i = 0; i < 8; ++i) counts[i] = g_cnt[i];
   return g_bad_bound;
 }
 
