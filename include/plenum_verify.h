@@ -168,7 +168,9 @@ int pv_keycache_size(uint64_t *count);
  * key.  A verify then needs 24 doublings and 32 key adds instead of 28 and 64;
  * the preparation costs ~16x the default format's, so it pays for keys that
  * sign many messages per preparation (a pool's node keys, C3).  Same verdicts.
- * Preparation runs 8 lanes per key (one per table).  Async forms as
+ * Preparation runs 128 lanes per key (16 slices of each of the 8 tables) and
+ * holds 160 KB of device scratch per key while it runs (128 lanes x 320 words,
+ * owned by the device context, grown to the largest k seen).  Async forms as
  * pv_*_device_async (slot 0 or 1, enqueue only). */
 #define PV_KEY_WORDS_WIDE 33056u
 int pv_keys_prepare_wide_device(const uint8_t *pk, uint64_t k, uint32_t *ktab, int device, void *stream);

@@ -1498,8 +1498,9 @@ int pv_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const 
   return PV_OK;
 }
 
-// wide key format (radix-256 comb): preparation on 8 lanes per key into
-// kscr / kscr2 (the slot's key scratch), verification through k_curve<true, 1>
+// wide key format (radix-256 comb): preparation on KEYTAB_WIDE_LANES (128) lanes
+// per key into kscr / kscr2 (the slot's key scratch, 160 KB per key), verification
+// through k_curve<true, 1>
 static int keys_prepare_wide(Device& d, const uint8_t* pk, uint64_t k, uint32_t* ktab, hipStream_t s, int slot) {
   int rc = ws_begin(d.ws[slot], s);
   if (rc) return rc;

@@ -25,6 +25,7 @@
 
 #include "../../include/plenum_verify.h"
 #include "pv_bn254.h"
+#include "pv_bn254_pair.h"
 #include "pv_sha256.h"
 
 // a named namespace: profilers show the kernels as pvbls::k_bls_*
@@ -36,13 +37,16 @@ constexpr int KEY_LINE_WORDS = N_LINES * LINE_WORDS;   // 2800 words per G2 poin
 constexpr int MSG_WORDS = 4 * NL;                        // x_H, y_H, xq(-H), yq(-H)
 constexpr int BLS_BLOCK = 256;
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(PV_BN_MILLER_REGS)
-static_assert(BLS_BLOCK == bn::MF_LANES, "the Miller loop's LDS accumulator is laid out per check block");
+static_assert(BLS_BLOCK == bn::MF_LANES && BLS_BLOCK == 2 * bn::MP_CHECKS,
+              "the Miller loop's LDS accumulator is laid out per check block");
 #endif
-// waves per SIMD the check kernel is compiled for: 1 (512 registers) measured
-// 1.77x the throughput of 2 (256 registers, the tower temporaries spill) on the
-// full C3-BLS batch (profiles/r03_ab_bls_waves.jsonl)
-#ifndef PV_BLS_WAVES
-#define PV_BLS_WAVES 1
+// the check kernel: one check per lane PAIR at 2 waves per SIMD
+// (k_bls_verify_pair, pv_bn254_pair.h); -DPV_BLS_ONE_LANE builds the one-lane
+// kernel k_bls_verify (512 registers, 1 wave per SIMD) for A/B timing
+#ifdef PV_BLS_ONE_LANE
+constexpr uint32_t BLS_WAVE_CHECKS = 64;   // checks per wave (= the key segments' padding)
+#else
+constexpr uint32_t BLS_WAVE_CHECKS = 32;
 #endif
 
 __device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
@@ -89,7 +93,7 @@ __global__ __launch_bounds__(64) void k_bls_hash(const uint8_t* __restrict__ blo
   st_fp(t + 3 * NL, yq);
 }
 
-// grouping by key: count, padded segment starts (64-aligned), scatter
+// grouping by key: count, padded segment starts (BLS_WAVE_CHECKS-aligned), scatter
 // a check whose key index is out of range is never scheduled: its verdict stays 0
 __global__ void k_bls_count(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys, uint32_t* __restrict__ cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -102,7 +106,7 @@ __global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uin
   uint32_t s = 0;
   for (uint32_t j = 0; j < k; ++j) {
     seg[j] = s;
-    s += (cnt[j] + 63u) & ~63u;
+    s += (cnt[j] + BLS_WAVE_CHECKS - 1) & ~(BLS_WAVE_CHECKS - 1);
   }
   *total = s;
 }
@@ -117,9 +121,10 @@ __global__ void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, 
   order[seg[key] + atomicAdd(cursor + key, 1u)] = (uint32_t)i;
 }
 
+#ifdef PV_BLS_ONE_LANE
 // one lane per check, one key per wave (slots of `order` padded to 64 per key;
 // 0xffffffff = idle lane, which computes on the point at infinity and writes nothing)
-__global__ __launch_bounds__(BLS_BLOCK, PV_BLS_WAVES) void k_bls_verify(
+__global__ __launch_bounds__(BLS_BLOCK, 1) void k_bls_verify(
     const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
     const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
     const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint32_t n_msgs,
@@ -148,6 +153,41 @@ __global__ __launch_bounds__(BLS_BLOCK, PV_BLS_WAVES) void k_bls_verify(
   const bool ok = bls_check(xs, ys, s_inf, xqh, yqh, st == 1, g_lines, pk_lines);
   if (live) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
 }
+#else
+// one check per lane PAIR (lanes 2c, 2c + 1), one key per wave (slots of
+// `order` padded to 32 per key; 0xffffffff = an idle pair, which computes on the
+// point at infinity and writes nothing).  Control flow is pair-uniform: both
+// lanes of a pair load the same check and take the same branches.
+__global__ __launch_bounds__(BLS_BLOCK, 2) void k_bls_verify_pair(
+    const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
+    const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint32_t n_msgs,
+    uint8_t* __restrict__ verdict) {
+  const uint32_t slot = (blockIdx.x * BLS_BLOCK + threadIdx.x) >> 1;
+  const uint32_t task0 = __builtin_amdgcn_readfirstlane(slot & ~(BLS_WAVE_CHECKS - 1));
+  if (task0 >= *total) return;   // whole wave: past the last padded segment
+  const uint32_t j = order[slot];
+  const bool live = j != 0xffffffffu;
+  // the first pair of a task is always live (segments fill from their start)
+  const uint32_t key = __builtin_amdgcn_readfirstlane(live ? key_idx[j] : 0u);
+  const uint32_t* g_lines = lines;
+  const uint32_t* pk_lines = lines + (uint64_t)KEY_LINE_WORDS * (1 + key);
+  const uint8_t st = kstatus[1 + key];
+  fp xs, ys, xqh = fzero(), yqh = fzero();
+  bool s_inf = true;
+  const bool msg_ok = live && msg_idx[j] < n_msgs;   // out of range: verdict 0
+  if (live) {
+    g1_decode(sig + 128ull * j, xs, ys, s_inf);
+    const uint32_t* t = msgtab + (uint64_t)MSG_WORDS * (msg_ok ? msg_idx[j] : 0u);
+    if (st == 0 && msg_ok) {
+      xqh = ld_fp(t + 2 * NL);
+      yqh = ld_fp(t + 3 * NL);
+    }
+  }
+  const bool ok = bls_check_pair(mp_slot(), xs, ys, s_inf, xqh, yqh, st == 1, g_lines, pk_lines);
+  if (live && !(threadIdx.x & 1)) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
+}
+#endif
 
 // Bls::verify_multi_sig's aggregated key (ursa: PointG2::new_inf() + every
 // ver_key.point): one lane per check sums its keys (each decoded as
@@ -344,9 +384,9 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
                    uint64_t n_msgs, const uint32_t* msg_idx, const uint32_t* key_idx, uint64_t n, uint8_t* verdict,
                    hipStream_t s) {
   if (!ks.nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", d.ord);
-  if (n > 0xffffffffull - 64ull * ks.nkeys) return bfail(PV_EINVAL, "too many checks in one call");
+  if (n > 0x7fffffffull - 64ull * ks.nkeys) return bfail(PV_EINVAL, "too many checks in one call");
   if (n_msgs > 0xffffffffull) return bfail(PV_EINVAL, "too many messages in one call");
-  const uint64_t slots = ((n + 63) / 64 + ks.nkeys) * 64;
+  const uint64_t slots = ((n + BLS_WAVE_CHECKS - 1) / BLS_WAVE_CHECKS + ks.nkeys) * BLS_WAVE_CHECKS;
   BLS_HIP(d.msgtab.ensure(n_msgs * MSG_WORDS));
   BLS_HIP(d.cnt.ensure(ks.nkeys));
   BLS_HIP(d.cursor.ensure(ks.nkeys));
@@ -368,8 +408,13 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
                      d.cursor.p, d.order.p);
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[2], s));
+#ifdef PV_BLS_ONE_LANE
   hipLaunchKernelGGL(k_bls_verify, dim3(blocks_for(slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx, key_idx,
                      d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs, verdict);
+#else
+  hipLaunchKernelGGL(k_bls_verify_pair, dim3(blocks_for(2 * slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx,
+                     key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs, verdict);
+#endif
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[3], s));
   return PV_OK;

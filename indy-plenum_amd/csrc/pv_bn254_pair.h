@@ -1,0 +1,569 @@
+// One BLS COMMIT check over a lane PAIR (the kernel
+// pvbls::k_bls_verify_pair).  The same check as bls_check (pv_bn254.h) --
+// e(sigma, g) e(-H(m), pk) == 1 over the precomputed lines, one final
+// exponentiation -- with every Fp12 split in halves between the two lanes:
+//   role h = 0 computes and writes the a-half (the Fp6 coefficient of w^0),
+//   role h = 1 the b-half (the coefficient of w),
+// and each lane's work per step is ONE Fp6 product of the complex squaring, ONE
+// sparse Fp6 product per line, three of the six Fp2 products of a cyclotomic
+// squaring, two of the four Fp6 products of an Fp12 product.  Half the work per
+// lane and half the registers: the kernel runs at 2 waves per SIMD (256
+// registers) where the one-lane check needs 512.
+//
+// The two lanes run the same instruction stream; a role only selects operands
+// (v_cndmask), never a branch, and the halves cross between the lanes with
+// quad_perm DPP moves (v_mov_dpp [1,0,3,2]) -- always in pair-uniform control
+// flow, so both lanes of a pair are active at every exchange.  The Miller
+// accumulator and the cyclotomic powers live in LDS, one Fp12 per check shared
+// by the pair (pslot); the final exponentiation's other values are halves in
+// registers (p6).
+//
+// The host build (tools/hostcheck/bn254check.cpp) compiles the same code with
+// both lanes of a pair emulated in one thread (PL = 2: element j plays role j,
+// an exchange swaps the elements), so the column-sum bound checker and the C
+// oracle cover exactly the formulas the kernel runs.
+#pragma once
+#include "pv_bn254.h"
+
+// member functions (PV_HD may be `static inline` in the host checker)
+#if defined(__HIPCC__)
+#define PV_MD __host__ __device__ __forceinline__
+#else
+#define PV_MD inline
+#endif
+
+namespace bn {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+constexpr int PL = 1;   // pair lanes held by one thread
+#else
+constexpr int PL = 2;
+#endif
+
+PV_HD int prole(int j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  (void)j;
+  return (int)(threadIdx.x & 1);
+#else
+  return j;
+#endif
+}
+
+struct p1 {
+  fp e[PL];
+};
+struct p2 {
+  fp2 e[PL];
+};
+struct p6 {
+  fp6 e[PL];
+};
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ fp px_fp(const fp& x) {   // the partner lane's x
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = __builtin_amdgcn_mov_dpp(x.l[i], 0xB1, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ fp2 px_fp2(const fp2& x) { return fp2{px_fp(x.a), px_fp(x.b)}; }
+#endif
+PV_HD p2 pswap(const p2& x) {
+  p2 r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  r.e[0] = px_fp2(x.e[0]);
+#else
+  r.e[0] = x.e[1];
+  r.e[1] = x.e[0];
+#endif
+  return r;
+}
+PV_HD p6 pswap(const p6& x) {
+  p6 r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  r.e[0] = fp6{px_fp2(x.e[0].c0), px_fp2(x.e[0].c1), px_fp2(x.e[0].c2)};
+#else
+  r.e[0] = x.e[1];
+  r.e[1] = x.e[0];
+#endif
+  return r;
+}
+// both lanes' flags ANDed
+PV_HD bool pand(const bool (&ok)[PL]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int o = __builtin_amdgcn_mov_dpp((int)ok[0], 0xB1, 0xf, 0xf, false);
+  return ok[0] && o;
+#else
+  return ok[0] && ok[1];
+#endif
+}
+
+PV_HD void mp_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" ::: "memory");
+#endif
+}
+
+// lazy (limbwise) helpers
+PV_HD fp2 f2negL(const fp2& x) { return fp2{neg(x.a), neg(x.b)}; }
+// role selects of values computed on both lanes (function arguments: both are
+// evaluated, so the choice is a v_cndmask, never a divergent branch)
+PV_HD fp fsel(bool h, const fp& x, const fp& y) { return h ? x : y; }
+PV_HD fp2 f2sel(bool h, const fp2& x, const fp2& y) { return h ? x : y; }
+PV_HD fp6 f6sel(bool h, const fp6& x, const fp6& y) { return h ? x : y; }
+
+// the pair kernel's block: 128 checks, f of check c at word w -> mp_buf[w * 128 + c]
+constexpr int MP_CHECKS = 128;
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ uint32_t mp_buf[12 * NL * MP_CHECKS];
+#endif
+
+// one check's Fp12 in LDS, shared by its pair: word w at mp_buf[w * ST + c] on
+// the device (indexed from the __shared__ array itself, so that every access is
+// a ds_read / ds_write, never a flat access through a generic pointer), at
+// p[w * ST] on the host (coefficient e = a.c0 a.c1 a.c2 b.c0 b.c1 b.c2 = 0..5,
+// each fp2 as a then b)
+//
+// Banks: ds_read_b32 / ds_write_b32 conflict within a 32-lane half (16 checks),
+// bank = dword address mod 32, and ST = 128 puts every word of check c on bank
+// c.  The lanes of a pair often touch different halves of their Fp12 in one
+// instruction (role 0 the b-half, role 1 the a-half), so the b-half of check c
+// is stored in column c ^ 16: the two roles then always use disjoint banks.
+template <int ST>
+struct pslot {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t c;
+  PV_MD uint32_t& at(int w, int e) const { return mp_buf[w * ST + (c ^ (e >= 3 ? 16u : 0u))]; }
+#else
+  uint32_t* p;
+  PV_MD uint32_t& at(int w, int) const { return p[w * ST]; }
+#endif
+  PV_MD fp2 ld(int e) const {
+    fp2 r;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      r.a.l[i] = (int32_t)at(2 * e * NL + i, e);
+      r.b.l[i] = (int32_t)at((2 * e + 1) * NL + i, e);
+    }
+    return r;
+  }
+  PV_MD void st(int e, const fp2& x) const {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      at(2 * e * NL + i, e) = (uint32_t)x.a.l[i];
+      at((2 * e + 1) * NL + i, e) = (uint32_t)x.b.l[i];
+    }
+  }
+  PV_MD fp6 ld6(int half) const { return fp6{ld(3 * half), ld(3 * half + 1), ld(3 * half + 2)}; }
+  PV_MD void st6(int half, const fp6& x) const {
+    st(3 * half, x.c0);
+    st(3 * half + 1, x.c1);
+    st(3 * half + 2, x.c2);
+  }
+};
+
+// x (the Fp6 half `half` of the slot) * (b0 + b1 v), each Fp2 of x fetched when
+// its product starts (f6mul01's sums)
+template <int ST>
+PV_HD fp6 mp_f6mul01(pslot<ST> S, int half, const fp2& b0, const fp2& b1) {
+  const int X = 3 * half;
+  const fp2 t0 = f2mul(S.ld(X), b0);
+  mp_fence();
+  const fp2 t1 = f2mul(S.ld(X + 1), b1);
+  mp_fence();
+  fp6 r;
+  {
+    const fp2 x2 = S.ld(X + 2);
+    r.c0 = f2norm(f2addL(t0, f2mulxiL(f2mul(x2, b1))));
+    r.c2 = f2norm(f2addL(t1, f2mul(x2, b0)));
+  }
+  mp_fence();
+  {
+    const fp2 m = f2mul(f2addL(S.ld(X), S.ld(X + 1)), f2add(b0, b1));
+    r.c1 = f2norm(f2subL(f2subL(m, t0), t1));
+  }
+  return r;
+}
+
+// f = f (1 + (b0 + b1 v) w), f12mul_line_i split: role 0 forms v (f.b l) and
+// writes f.a + v f.b l, role 1 forms f.a l and writes f.b + f.a l.  The line's
+// coefficients b0 = B' x_P (role 0) and b1 = C' y_P (role 1) are exchanged;
+// q holds each role's coordinate of P (x_P for role 0, y_P for role 1).
+template <int ST>
+PV_HD void mp_line(pslot<ST> S, const uint32_t* L, const p1& q) {
+  p2 c;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) c.e[j] = f2mulfp(ld_f2(L + 2 * NL * prole(j)), q.e[j]);
+  const p2 o = pswap(c);
+  p6 P;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+    const fp2 b0 = f2sel(h, o.e[j], c.e[j]), b1 = f2sel(h, c.e[j], o.e[j]);
+    P.e[j] = mp_f6mul01(S, 1 - h, b0, b1);
+  }
+  mp_fence();
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j), E = 3 * h;
+    const fp6& t = P.e[j];
+    const fp2 q0 = f2sel(h, t.c0, f2mulxiL(t.c2)), q1 = f2sel(h, t.c1, t.c0), q2 = f2sel(h, t.c2, t.c1);
+    S.st(E, f2norm(f2addL(S.ld(E), q0)));
+    S.st(E + 1, f2norm(f2addL(S.ld(E + 1), q1)));
+    S.st(E + 2, f2norm(f2addL(S.ld(E + 2), q2)));
+  }
+  mp_fence();
+}
+
+// f = f^2 (f12sqr_i's complex squaring split): role 0 forms s = (a + b)(a + v b),
+// role 1 t = a b; t crosses to role 0, which writes s - t - v t, role 1 writes
+// 2t (as p - (-p) - 0, the same integer as f2dbl)
+template <int ST>
+PV_HD fp6 mp_sqr_prod(pslot<ST> S, int h) {
+  fp6 x, y;
+  {
+    const fp6 a = S.ld6(0), b = S.ld6(1);
+    x = f6sel(h, a, f6add(a, b));
+    y = f6sel(h, b, f6add(a, f6mulv(b)));
+  }
+  return f6mul_i(x, y);
+}
+template <int ST>
+PV_HD void mp_sqr(pslot<ST> S) {
+  p6 P;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) P.e[j] = mp_sqr_prod(S, prole(j));
+  mp_fence();
+  const p6 Q = pswap(P);
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+    const fp6& p = P.e[j];
+    const fp6& q = Q.e[j];
+    const fp2 z = f2zero();
+    const fp2 a0 = f2sel(h, f2negL(p.c0), q.c0), a1 = f2sel(h, f2negL(p.c1), q.c1), a2 = f2sel(h, f2negL(p.c2), q.c2);
+    const fp2 c0 = f2sel(h, z, f2mulxiL(q.c2)), c1 = f2sel(h, z, q.c0), c2 = f2sel(h, z, q.c1);
+    S.st6(h, fp6{f2norm(f2subL(f2subL(p.c0, a0), c0)), f2norm(f2subL(f2subL(p.c1, a1), c1)),
+                 f2norm(f2subL(f2subL(p.c2, a2), c2))});
+  }
+  mp_fence();
+}
+
+// cyc_sqr_i split: of each Fp4 pair (z0, z1) -- A = (a.c0, b.c1), B = (b.c0,
+// a.c2), C = (a.c1, b.c2) -- role 0 forms s = (z0 + z1)(xi z1 + z0), role 1
+// tmp = z0 z1; tmp crosses to role 0.  Role 0 writes a.c0, a.c1, a.c2 =
+// 3 t0 - 2 z (t0 = s - tmp - xi tmp of A, B, C), role 1 writes b.c1, b.c2,
+// b.c0 = 3 t1 + 2 z (t1 = 2 tmp of A, B and xi 2 tmp of C).  Every sum is formed
+// limbwise (|limb| < 2^31) and carried once: the same integers as fp4_sqr /
+// three_minus_two / three_plus_two, so the same normalised limbs.
+template <int ST>
+PV_HD void mp_cyc_sqr(pslot<ST> S) {
+  constexpr int Z0[3] = {0, 3, 1}, Z1[3] = {4, 2, 5}, O0[3] = {0, 1, 2}, O1[3] = {4, 5, 3};
+  p2 P[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int h = prole(j);
+      const fp2 z0 = S.ld(Z0[k]), z1 = S.ld(Z1[k]);
+      const fp2 x = f2sel(h, z0, f2addL(z0, z1));                    // lazy factor
+      const fp2 y = f2sel(h, z1, f2norm(f2addL(f2mulxiL(z1), z0)));   // normalised factor
+      P[k].e[j] = f2mul(x, y);
+    }
+    mp_fence();
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const p2 Q = pswap(P[k]);
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int h = prole(j);
+      const fp2& p = P[k].e[j];
+      // u = a - b - c: role 0 s - tmp - xi tmp, role 1 2 tmp = a - (-a) - 0 (a = xi tmp for C)
+      const fp2 a = k == 2 ? f2sel(h, f2mulxiL(p), p) : p;
+      const fp2 u = f2norm(f2subL(f2subL(a, f2sel(h, f2negL(a), Q.e[j])), f2sel(h, f2zero(), f2mulxiL(Q.e[j]))));
+      const int e = h ? O1[k] : O0[k];
+      const fp2 zz = S.ld(e);
+      const fp2 zs = f2sel(h, zz, f2negL(zz));   // 3u - 2z (role 0) / 3u + 2z (role 1)
+      S.st(e, f2norm(f2addL(f2addL(f2addL(u, u), u), f2addL(zs, zs))));
+    }
+  }
+  mp_fence();
+}
+template <int ST>
+PV_HD void mp_reduce(pslot<ST> S) {
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) S.st(3 * h + k, f2reduce(S.ld(3 * h + k)));
+  }
+  mp_fence();
+}
+template <int ST>
+PV_HD void mp_put(pslot<ST> S, const p6& x) {
+#pragma unroll
+  for (int j = 0; j < PL; ++j) S.st6(prole(j), x.e[j]);
+  mp_fence();
+}
+template <int ST>
+PV_HD p6 mp_get(pslot<ST> S) {
+  p6 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) r.e[j] = S.ld6(prole(j));
+  return r;
+}
+
+// ------------------------------------------------------------------ Fp12 halves (p6)
+// x y, f12mul's Karatsuba split: role 0 forms t0 = x.a y.a, role 1 t1 = x.b y.b
+// (one Fp6 product each, from the lane's own halves); the third product s =
+// (x.a + x.b)(y.a + y.b) is split at the Fp2 level -- role 0 forms its v0, v1,
+// v2, role 1 its s12, s01, s02.  Role 0 writes t0 + v t1, role 1 s - t0 - t1:
+// the same sums as f12mul, so the same limbs.
+PV_BN_CALL p6 pr_mul(const p6& x, const p6& y) {
+  p6 t;   // the out-of-line product first: nothing else is live across the call
+#pragma unroll
+  for (int j = 0; j < PL; ++j) t.e[j] = f6mul(x.e[j], y.e[j]);
+  p2 m[3];
+  {
+    const p6 xo = pswap(x), yo = pswap(y);
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int h = prole(j);
+      const fp6 X = f6add(x.e[j], xo.e[j]), Y = f6add(y.e[j], yo.e[j]);
+      // role 0: X_k Y_k (k = 0, 1, 2); role 1: (X_a + X_b)(Y_a + Y_b) for (a, b) = (1, 2), (0, 1), (0, 2)
+      m[0].e[j] = f2mul(f2sel(h, f2addL(X.c1, X.c2), X.c0), f2sel(h, f2add(Y.c1, Y.c2), Y.c0));
+      m[1].e[j] = f2mul(f2sel(h, f2addL(X.c0, X.c1), X.c1), f2sel(h, f2add(Y.c0, Y.c1), Y.c1));
+      m[2].e[j] = f2mul(f2sel(h, f2addL(X.c0, X.c2), X.c2), f2sel(h, f2add(Y.c0, Y.c2), Y.c2));
+    }
+  }
+  const p6 to = pswap(t);
+  const p2 mo[3] = {pswap(m[0]), pswap(m[1]), pswap(m[2])};
+  p6 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+    const fp6& t0 = h ? to.e[j] : t.e[j];
+    const fp6& t1 = h ? t.e[j] : to.e[j];
+    // s (role 1's view: v's from role 0)
+    const fp2 &v0 = mo[0].e[j], &v1 = mo[1].e[j], &v2 = mo[2].e[j];
+    const fp2 &s12 = m[0].e[j], &s01 = m[1].e[j], &s02 = m[2].e[j];
+    const fp2 sc0 = f2norm(f2addL(f2mulxiL(f2subL(f2subL(s12, v1), v2)), v0));
+    const fp2 sc1 = f2norm(f2addL(f2subL(f2subL(s01, v0), v1), f2mulxiL(v2)));
+    const fp2 sc2 = f2norm(f2addL(f2subL(f2subL(s02, v0), v2), v1));
+    const fp6 rb{f2norm(f2subL(f2subL(sc0, t0.c0), t1.c0)), f2norm(f2subL(f2subL(sc1, t0.c1), t1.c1)),
+                 f2norm(f2subL(f2subL(sc2, t0.c2), t1.c2))};
+    const fp6 ra{f2norm(f2addL(t0.c0, f2mulxiL(t1.c2))), f2norm(f2addL(t0.c1, t1.c0)), f2norm(f2addL(t0.c2, t1.c1))};
+    r.e[j] = f6sel(h, rb, ra);
+  }
+  return r;
+}
+PV_HD p6 pr_conj(const p6& x) {
+  p6 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) r.e[j] = f6sel(prole(j), f6neg(x.e[j]), x.e[j]);
+  return r;
+}
+// 1 / x = (a - b w) / (a^2 - v b^2): role 0 squares a, role 1 b; both invert
+// the same Fp6 norm
+PV_BN_CALL p6 pr_inv(const p6& x) {
+  p6 sq;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) sq.e[j] = f6mul(x.e[j], x.e[j]);
+  const p6 so = pswap(sq);
+  p6 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+    const fp6 d = f6inv(f6sub(f6sel(h, so.e[j], sq.e[j]), f6mulv(f6sel(h, sq.e[j], so.e[j]))));
+    const fp6 m = f6mul(x.e[j], d);
+    r.e[j] = f6sel(h, f6neg(m), m);
+  }
+  return r;
+}
+// Frobenius maps on the lane's own coefficients (f12frob1/2/3): role 0 holds
+// w^0, w^2, w^4 (gamma_{n,0} = 1, gamma_{n,2}, gamma_{n,4}), role 1 w^1, w^3,
+// w^5 -- one multiply per coefficient with the role's constant (role 0 times
+// the Montgomery one for w^0)
+PV_HD p6 pr_frob_odd(const p6& x, int n, const uint32_t* const (&g)[10]) {
+  p6 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+    const fp6& c = x.e[j];
+    const fp2 one = f2one();
+    r.e[j].c0 = f2mul(f2conj(c.c0), f2sel(h, f2cst(g[0], g[1]), one));
+    r.e[j].c1 = f2mul(f2conj(c.c1), f2sel(h, f2cst(g[4], g[5]), f2cst(g[2], g[3])));
+    r.e[j].c2 = f2mul(f2conj(c.c2), f2sel(h, f2cst(g[8], g[9]), f2cst(g[6], g[7])));
+  }
+  (void)n;
+  return r;
+}
+PV_BN_CALL p6 pr_frob1(const p6& x) {
+  const uint32_t* const g[10] = {G1_1_A, G1_1_B, G1_2_A, G1_2_B, G1_3_A, G1_3_B, G1_4_A, G1_4_B, G1_5_A, G1_5_B};
+  return pr_frob_odd(x, 1, g);
+}
+PV_BN_CALL p6 pr_frob3(const p6& x) {
+  const uint32_t* const g[10] = {G3_1_A, G3_1_B, G3_2_A, G3_2_B, G3_3_A, G3_3_B, G3_4_A, G3_4_B, G3_5_A, G3_5_B};
+  return pr_frob_odd(x, 3, g);
+}
+PV_BN_CALL p6 pr_frob2(const p6& x) {
+  p6 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+    const fp6& c = x.e[j];
+    r.e[j].c0 = f2mulfp(c.c0, fsel(h, cst(G2_1_A), fone()));
+    r.e[j].c1 = f2mulfp(c.c1, fsel(h, cst(G2_3_A), cst(G2_2_A)));
+    r.e[j].c2 = f2mulfp(c.c2, fsel(h, cst(G2_5_A), cst(G2_4_A)));
+  }
+  return r;
+}
+PV_HD bool pr_is_one(const p6& x) {
+  bool ok[PL];
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const fp6& c = x.e[j];
+    const bool rest = f2is_zero(c.c1) && f2is_zero(c.c2) && is_zero(c.c0.b);
+    ok[j] = rest && (prole(j) ? is_zero(c.c0.a) : eq(c.c0.a, fone()));
+  }
+  return pand(ok);
+}
+
+// x^u in the cyclotomic subgroup (cyc_pow_u's chain) with the power in the slot
+template <int ST>
+PV_BN_CALL p6 pr_pow_u(pslot<ST> S, const p6& x) {
+  mp_put(S, x);
+  for (int i = 0; i < 7; ++i) {
+    mp_cyc_sqr(S);
+    if ((i & 3) == 3) mp_reduce(S);
+  }
+  mp_put(S, pr_mul(mp_get(S), x));   // x^(2^7 + 1)
+  for (int i = 0; i < 55; ++i) {
+    mp_cyc_sqr(S);
+    if ((i & 3) == 3) mp_reduce(S);
+  }
+  return pr_conj(pr_mul(mp_get(S), x));   // x^(2^62 + 2^55 + 1), conjugated
+}
+template <int ST>
+PV_BN_CALL p6 pr_cyc_sqr(pslot<ST> S, const p6& x) {
+  mp_put(S, x);
+  mp_cyc_sqr(S);
+  return mp_get(S);
+}
+
+// final_exp's chain on halves
+template <int ST>
+PV_BN_CALL p6 pr_final_exp(pslot<ST> S, const p6& f0) {
+  p6 f = pr_mul(pr_conj(f0), pr_inv(f0));   // ^(p^6 - 1)
+  f = pr_mul(pr_frob2(f), f);              // ^(p^2 + 1)
+  const p6 fu = pr_pow_u(S, f);
+  const p6 fu2 = pr_pow_u(S, fu);
+  const p6 fu3 = pr_pow_u(S, fu2);
+  const p6 y6 = pr_conj(pr_mul(fu3, pr_frob1(fu3)));
+  p6 t0 = pr_cyc_sqr(S, y6);
+  t0 = pr_mul(t0, pr_conj(pr_mul(fu, pr_frob1(fu2))));   // y4
+  const p6 y5 = pr_conj(fu2);
+  t0 = pr_mul(t0, y5);
+  p6 t1 = pr_mul(pr_mul(pr_conj(pr_frob1(fu)), y5), t0);
+  t0 = pr_mul(t0, pr_frob2(fu2));
+  t1 = pr_mul(pr_cyc_sqr(S, t1), t0);
+  t1 = pr_cyc_sqr(S, t1);
+  t0 = pr_mul(t1, pr_conj(f));
+  const p6 y0 = pr_mul(pr_mul(pr_frob1(f), pr_frob2(f)), pr_frob3(f));
+  t1 = pr_mul(t1, y0);
+  return pr_mul(pr_cyc_sqr(S, t0), t1);
+}
+
+#if defined(__HIPCC__)
+// this lane's check slot (lanes 2c and 2c + 1 share check c of the block)
+__device__ __forceinline__ pslot<MP_CHECKS> mp_slot() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return pslot<MP_CHECKS>{threadIdx.x >> 1};
+#else
+  return pslot<MP_CHECKS>{nullptr};
+#endif
+}
+#endif
+
+// the two-pairing Miller product into the slot (miller2's steps); returns f's halves
+template <int ST>
+PV_BN_CALL p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_lines, const fp* xq,
+                          const fp* yq) {
+  p1 q[2];   // the lane's coordinate of each G1 point (x/y for role 0, 1/y for role 1)
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    q[0].e[j] = fsel(prole(j), yq[0], xq[0]);
+    q[1].e[j] = fsel(prole(j), yq[1], xq[1]);
+    S.st6(prole(j), prole(j) ? f6zero() : f6one());
+  }
+  mp_fence();
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the step's two lines staged per wave in LDS (one key per wave), one step ahead
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  uint32_t pg = 0, pp = 0;
+  auto fetch = [&](int kk) {
+    if (ln < LINE_WORDS && kk < N_LINES) {
+      pg = g_lines[LINE_WORDS * kk + ln];
+      pp = pk_lines[LINE_WORDS * kk + ln];
+    }
+  };
+  auto stash = [&](int kk) {
+    if (ln < LINE_WORDS && kk < N_LINES) {
+      mf_lines[wv][kk & 1][0][ln] = pg;
+      mf_lines[wv][kk & 1][1][ln] = pp;
+    }
+    mp_fence();
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto Lg = [&](int kk) -> const uint32_t* { return mf_lines[wv][kk & 1][0]; };
+  auto Lp = [&](int kk) -> const uint32_t* { return mf_lines[wv][kk & 1][1]; };
+  fetch(0);
+  stash(0);
+#else
+  auto fetch = [](int) {};
+  auto stash = [](int) {};
+  auto Lg = [&](int kk) -> const uint32_t* { return g_lines + LINE_WORDS * kk; };
+  auto Lp = [&](int kk) -> const uint32_t* { return pk_lines + LINE_WORDS * kk; };
+#endif
+  int k = 0;
+  for (int i = 63; i >= 0; --i) {
+    for (int add = 0; add < 2; ++add) {
+      if (add && !ate_bit(i)) break;
+      fetch(k + 1);
+      if (!add && i != 63) mp_sqr(S);
+      mp_line(S, Lg(k), q[0]);
+      mp_line(S, Lp(k), q[1]);
+      stash(k + 1);
+      ++k;
+    }
+  }
+  mp_put(S, pr_conj(mp_get(S)));
+  for (int j = 0; j < 2; ++j, ++k) {
+    fetch(k + 1);
+    mp_line(S, Lg(k), q[0]);
+    mp_line(S, Lp(k), q[1]);
+    stash(k + 1);
+  }
+  return mp_get(S);
+}
+
+// bls_check over the pair (both lanes return the verdict)
+template <int ST>
+PV_HD bool bls_check_pair(pslot<ST> S, const fp& xs, const fp& ys, bool s_inf, const fp& xqh, const fp& yqh,
+                          bool pk_inf, const uint32_t* g_lines, const uint32_t* pk_lines) {
+  fp xq[2], yq[2];
+  if (s_inf) {
+    xq[0] = fzero();
+    yq[0] = fzero();
+  } else {
+    line_point(xs, ys, false, xq[0], yq[0]);
+  }
+  xq[1] = xqh;
+  yq[1] = yqh;
+  const bool one = pr_is_one(pr_final_exp(S, miller_pair(S, g_lines, pk_lines, xq, yq)));
+  if (s_inf || pk_inf) return s_inf && pk_inf;
+  return one;
+}
+
+}  // namespace bn

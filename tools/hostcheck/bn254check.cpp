@@ -25,6 +25,7 @@ static void bn_check_mul(const int32_t* a, const int32_t* b);
 #define PV_BN_CHECK_MUL(a, b) bn_check_mul((a).l, (b).l)
 
 #include "../../indy-plenum_amd/csrc/pv_bn254.h"
+#include "../../indy-plenum_amd/csrc/pv_bn254_pair.h"
 #include "../../indy-plenum_amd/csrc/pv_sha256.h"
 
 #include <math.h>
@@ -126,6 +127,29 @@ int bnc_verify(const uint8_t* sig128, const uint8_t* m, uint64_t n, const uint8_
   bool s_inf;
   g1_decode(sig128, xs, ys, s_inf);
   return bls_check(xs, ys, s_inf, xqh, yqh, st == 1, gl, pl) ? 1 : 0;
+}
+
+// the same check on the lane-pair kernel's schedule (pv_bn254_pair.h, both
+// lanes emulated; the slot is the check's LDS Fp12)
+int bnc_verify_pair(const uint8_t* sig128, const uint8_t* m, uint64_t n, const uint8_t* pk128, const uint8_t* gen128) {
+  static uint32_t gl[N_LINES * LINE_WORDS], pl[N_LINES * LINE_WORDS];
+  if (bnc_g2_lines(gen128, gl) != 0) return -1;
+  g2a q;
+  const int st = g2_decode(pk128, q);
+  if (st == 0) g2_lines(pl, q);
+  else memset(pl, 0, sizeof pl);
+  uint8_t h[128];
+  bnc_hash_to_g1(m, n, h);
+  const fp hx = to_mont(from_be32(h + 1)), hy = to_mont(from_be32(h + 33));
+  fp xqh, yqh;
+  line_point(hx, hy, true, xqh, yqh);
+  if (st != 0) xqh = yqh = fzero();
+  fp xs, ys;
+  bool s_inf;
+  g1_decode(sig128, xs, ys, s_inf);
+  uint32_t slot[12 * NL];
+  const pslot<1> S{slot};
+  return bls_check_pair(S, xs, ys, s_inf, xqh, yqh, st == 1, gl, pl) ? 1 : 0;
 }
 
 // the Fp multiplies / squarings of ONE check as k_bls_verify runs it (sigma
