@@ -543,14 +543,16 @@ def main_bls(args):
                    .format(nb), 'name': 'c3bls', 'checks': n, 'batches': nb},
         'verdict_mismatches': mism, 'quorum_mismatches': q_mism, 'quorums_reached': int(reached.sum().item()),
         'kernel_ms': {'hash': round(hash_ms, 3), 'verify': round(verify_ms, 3)},
-        'roofline': {'bound': 'valu', 'kernel': 'k_bls_verify', 'achieved': round(achieved / 1e12, 3),
+        'roofline': {'bound': 'valu', 'kernel': 'k_bls_verify_pair (+ k_bls_sigprep)', 'achieved': round(achieved / 1e12, 3),
                      'peak': round(peak / 1e12, 3), 'unit': 'T v_mad lane-ops/s', 'frac': round(achieved / peak, 4),
                      'work_per_check': BLS_W_MAD,
                      'traffic': (round(_pmc(BLS_PMC, 'hbm_bytes_per_unit') * n, 1)
                                  if _pmc(BLS_PMC, 'hbm_bytes_per_unit') else None),
                      'traffic_source': 'HBM bytes per check from rocprofv3 FETCH_SIZE / WRITE_SIZE passes '
                                        '(profiles/r04_bls_pmc.json) x the checks of this launch',
-                     'note': 'W = {} Fp mul x 180 + {} sqr x 135 v_mad_i64_i32 per check (host op counts)'
+                     'note': 'W = {} Fp mul x 180 + {} sqr x 135 v_mad_i64_i32 per check (host op counts of '
+                             'the one-lane schedule; the lane pair repeats the inversion of the final '
+                             'exponentiation on both lanes, not counted); time = the sigma-prep + pair kernels'
                              .format(BLS_W_MUL, BLS_W_SQR)},
     }
     # the per-COMMIT regime: host calls of 1 check, one 3PC batch (25 COMMITs,

@@ -154,6 +154,27 @@ __global__ __launch_bounds__(BLS_BLOCK, 1) void k_bls_verify(
   if (live) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
 }
 #else
+// sigma's line point per check, one lane per check (the pair kernel would run
+// this chain -- decoding, one inversion -- on both lanes of a pair): word w of
+// check i at prep[w * n + i], w = 0..9 x/y, 10..19 1/y, 20 = 1 if sigma decodes
+// to the point at infinity
+constexpr int SIGPREP_WORDS = 2 * NL + 1;
+__global__ __launch_bounds__(64) void k_bls_sigprep(const uint8_t* __restrict__ sig, uint64_t n,
+                                                    uint32_t* __restrict__ prep) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fp xs, ys, xq = fzero(), yq = fzero();
+  bool inf;
+  g1_decode(sig + 128ull * i, xs, ys, inf);
+  if (!inf) line_point(xs, ys, false, xq, yq);
+#pragma unroll
+  for (int w = 0; w < NL; ++w) {
+    prep[w * n + i] = (uint32_t)xq.l[w];
+    prep[(NL + w) * n + i] = (uint32_t)yq.l[w];
+  }
+  prep[2 * NL * n + i] = inf ? 1u : 0u;
+}
+
 // one check per lane PAIR (lanes 2c, 2c + 1), one key per wave (slots of
 // `order` padded to 32 per key; 0xffffffff = an idle pair, which computes on the
 // point at infinity and writes nothing).  Control flow is pair-uniform: both
@@ -162,8 +183,9 @@ __global__ __launch_bounds__(BLS_BLOCK, 2) void k_bls_verify_pair(
     const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
     const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
     const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint32_t n_msgs,
-    uint8_t* __restrict__ verdict) {
+    const uint32_t* __restrict__ prep, uint64_t n, uint8_t* __restrict__ verdict) {
   const uint32_t slot = (blockIdx.x * BLS_BLOCK + threadIdx.x) >> 1;
+  const int h = threadIdx.x & 1;
   const uint32_t task0 = __builtin_amdgcn_readfirstlane(slot & ~(BLS_WAVE_CHECKS - 1));
   if (task0 >= *total) return;   // whole wave: past the last padded segment
   const uint32_t j = order[slot];
@@ -173,19 +195,19 @@ __global__ __launch_bounds__(BLS_BLOCK, 2) void k_bls_verify_pair(
   const uint32_t* g_lines = lines;
   const uint32_t* pk_lines = lines + (uint64_t)KEY_LINE_WORDS * (1 + key);
   const uint8_t st = kstatus[1 + key];
-  fp xs, ys, xqh = fzero(), yqh = fzero();
+  // this lane's coordinate of each line point: x/y (role 0) or 1/y (role 1)
+  p1 q[2] = {{fzero()}, {fzero()}};
   bool s_inf = true;
   const bool msg_ok = live && msg_idx[j] < n_msgs;   // out of range: verdict 0
   if (live) {
-    g1_decode(sig + 128ull * j, xs, ys, s_inf);
+#pragma unroll
+    for (int w = 0; w < NL; ++w) q[0].e[0].l[w] = (int32_t)prep[(h * NL + w) * n + j];
+    s_inf = prep[2 * NL * n + j] != 0;
     const uint32_t* t = msgtab + (uint64_t)MSG_WORDS * (msg_ok ? msg_idx[j] : 0u);
-    if (st == 0 && msg_ok) {
-      xqh = ld_fp(t + 2 * NL);
-      yqh = ld_fp(t + 3 * NL);
-    }
+    if (st == 0 && msg_ok) q[1].e[0] = ld_fp(t + (2 + h) * NL);
   }
-  const bool ok = bls_check_pair(mp_slot(), xs, ys, s_inf, xqh, yqh, st == 1, g_lines, pk_lines);
-  if (live && !(threadIdx.x & 1)) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
+  const bool ok = bls_check_pair_q(mp_slot(), q, s_inf, st == 1, g_lines, pk_lines);
+  if (live && !h) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
 }
 #endif
 
@@ -340,7 +362,7 @@ struct BlsDev {
   KeySet keys;                    // pv_bls_set_keys
   KeySet multi;                   // per call of pv_bls_verify_multi_batch
   // per-call workspaces
-  Buf<uint32_t> msgtab, cnt, seg, cursor, order, total, midx, kidx;
+  Buf<uint32_t> msgtab, cnt, seg, cursor, order, total, midx, kidx, sigprep;
   Buf<uint8_t> sig, blob, verdict, sks, mpks;
   Buf<uint64_t> off, moff;
   float ms_hash = 0, ms_verify = 0;
@@ -393,6 +415,9 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   BLS_HIP(d.seg.ensure(ks.nkeys));
   BLS_HIP(d.total.ensure(1));
   BLS_HIP(d.order.ensure(slots));
+#ifndef PV_BLS_ONE_LANE
+  BLS_HIP(d.sigprep.ensure(n * SIGPREP_WORDS));
+#endif
   BLS_HIP(hipEventRecord(d.ev[0], s));
   if (n_msgs) hipLaunchKernelGGL(k_bls_hash, dim3(blocks_for(n_msgs, 64)), dim3(64), 0, s, blob, off, (uint32_t)n_msgs,
                                  d.msgtab.p);
@@ -412,8 +437,10 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   hipLaunchKernelGGL(k_bls_verify, dim3(blocks_for(slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx, key_idx,
                      d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs, verdict);
 #else
+  if (n) hipLaunchKernelGGL(k_bls_sigprep, dim3(blocks_for(n, 64)), dim3(64), 0, s, sig, n, d.sigprep.p);
   hipLaunchKernelGGL(k_bls_verify_pair, dim3(blocks_for(2 * slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx,
-                     key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs, verdict);
+                     key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs,
+                     d.sigprep.p, n, verdict);
 #endif
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[3], s));

@@ -104,6 +104,18 @@ PV_HD void mp_fence() {
 #endif
 }
 
+// pin an Fp2 product's limbs in 32-bit registers: left alone, the compiler sinks
+// a product's final column masks / carries to the (distant) uses and keeps the
+// 64-bit column sums alive instead -- twice the registers -- which spilled the
+// Miller loop to scratch at every line
+PV_HD fp2 pin(fp2 x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+  for (int i = 0; i < NL; ++i) asm volatile("" : "+v"(x.a.l[i]), "+v"(x.b.l[i]));
+#endif
+  return x;
+}
+
 // lazy (limbwise) helpers
 PV_HD fp2 f2negL(const fp2& x) { return fp2{neg(x.a), neg(x.b)}; }
 // role selects of values computed on both lanes (function arguments: both are
@@ -163,26 +175,60 @@ struct pslot {
 };
 
 // x (the Fp6 half `half` of the slot) * (b0 + b1 v), each Fp2 of x fetched when
-// its product starts (f6mul01's sums)
+// its product starts: f6mul01's five products folded into lazy output sums as
+// they are formed (c0 = t0 + xi t3, c1 = m - t0 - t1, c2 = t1 + t2; |limb| <
+// 3 * 2^28); the sum's product first, then b1's two, then b0's
 template <int ST>
 PV_HD fp6 mp_f6mul01(pslot<ST> S, int half, const fp2& b0, const fp2& b1) {
   const int X = 3 * half;
-  const fp2 t0 = f2mul(S.ld(X), b0);
-  mp_fence();
-  const fp2 t1 = f2mul(S.ld(X + 1), b1);
-  mp_fence();
-  fp6 r;
-  {
-    const fp2 x2 = S.ld(X + 2);
-    r.c0 = f2norm(f2addL(t0, f2mulxiL(f2mul(x2, b1))));
-    r.c2 = f2norm(f2addL(t1, f2mul(x2, b0)));
-  }
+  fp2 c0, c1, c2;
+  c1 = pin(f2mul(f2addL(S.ld(X), S.ld(X + 1)), f2add(b0, b1)));
   mp_fence();
   {
-    const fp2 m = f2mul(f2addL(S.ld(X), S.ld(X + 1)), f2add(b0, b1));
-    r.c1 = f2norm(f2subL(f2subL(m, t0), t1));
+    const fp2 t1 = pin(f2mul(S.ld(X + 1), b1));
+    c1 = f2subL(c1, t1);
+    c2 = t1;
   }
-  return r;
+  mp_fence();
+  c0 = f2mulxiL(pin(f2mul(S.ld(X + 2), b1)));
+  mp_fence();
+  {
+    const fp2 t0 = pin(f2mul(S.ld(X), b0));
+    c0 = f2addL(c0, t0);
+    c1 = f2subL(c1, t0);
+  }
+  mp_fence();
+  c2 = f2addL(c2, pin(f2mul(S.ld(X + 2), b0)));
+  return fp6{f2norm(c0), f2norm(c1), f2norm(c2)};
+}
+
+// f6mul_i(x, y) with each Fp2 product folded into the three lazy output sums as
+// it is formed (|limb| < 7 * 2^28 as in f6mul_i) instead of holding all six
+PV_HD fp6 f6mul_fold(const fp6& x, const fp6& y) {
+  fp2 c0, c1, c2;
+  {
+    const fp2 v0 = pin(f2mul(x.c0, y.c0));
+    c0 = v0;
+    c1 = f2negL(v0);
+    c2 = f2negL(v0);
+  }
+  {
+    const fp2 v1 = pin(f2mul(x.c1, y.c1));
+    c0 = f2subL(c0, f2mulxiL(v1));
+    c1 = f2subL(c1, v1);
+    c2 = f2addL(c2, v1);
+  }
+  {
+    const fp2 v2 = pin(f2mul(x.c2, y.c2));
+    const fp2 xv2 = f2mulxiL(v2);
+    c0 = f2subL(c0, xv2);
+    c1 = f2addL(c1, xv2);
+    c2 = f2subL(c2, v2);
+  }
+  c0 = f2addL(c0, f2mulxiL(pin(f2mul(f2addL(x.c1, x.c2), f2add(y.c1, y.c2)))));
+  c1 = f2addL(c1, pin(f2mul(f2addL(x.c0, x.c1), f2add(y.c0, y.c1))));
+  c2 = f2addL(c2, pin(f2mul(f2addL(x.c0, x.c2), f2add(y.c0, y.c2))));
+  return fp6{f2norm(c0), f2norm(c1), f2norm(c2)};
 }
 
 // f = f (1 + (b0 + b1 v) w), f12mul_line_i split: role 0 forms v (f.b l) and
@@ -193,7 +239,7 @@ template <int ST>
 PV_HD void mp_line(pslot<ST> S, const uint32_t* L, const p1& q) {
   p2 c;
 #pragma unroll
-  for (int j = 0; j < PL; ++j) c.e[j] = f2mulfp(ld_f2(L + 2 * NL * prole(j)), q.e[j]);
+  for (int j = 0; j < PL; ++j) c.e[j] = pin(f2mulfp(ld_f2(L + 2 * NL * prole(j)), q.e[j]));
   const p2 o = pswap(c);
   p6 P;
 #pragma unroll
@@ -226,7 +272,7 @@ PV_HD fp6 mp_sqr_prod(pslot<ST> S, int h) {
     x = f6sel(h, a, f6add(a, b));
     y = f6sel(h, b, f6add(a, f6mulv(b)));
   }
-  return f6mul_i(x, y);
+  return f6mul_fold(x, y);
 }
 template <int ST>
 PV_HD void mp_sqr(pslot<ST> S) {
@@ -268,7 +314,7 @@ PV_HD void mp_cyc_sqr(pslot<ST> S) {
       const fp2 z0 = S.ld(Z0[k]), z1 = S.ld(Z1[k]);
       const fp2 x = f2sel(h, z0, f2addL(z0, z1));                    // lazy factor
       const fp2 y = f2sel(h, z1, f2norm(f2addL(f2mulxiL(z1), z0)));   // normalised factor
-      P[k].e[j] = f2mul(x, y);
+      P[k].e[j] = pin(f2mul(x, y));
     }
     mp_fence();
   }
@@ -487,16 +533,14 @@ __device__ __forceinline__ pslot<MP_CHECKS> mp_slot() {
 #endif
 
 // the two-pairing Miller product into the slot (miller2's steps); returns f's halves
+// (q: the lane's coordinate of each G1 point, x/y for role 0 and 1/y for role 1).
+// Inlined into the kernel (one call site): as an out-of-line function its
+// wave-uniform arguments (the line pointers) lived in VGPRs and went through
+// scratch at every step.
 template <int ST>
-PV_BN_CALL p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_lines, const fp* xq,
-                          const fp* yq) {
-  p1 q[2];   // the lane's coordinate of each G1 point (x/y for role 0, 1/y for role 1)
+PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_lines, const p1 (&q)[2]) {
 #pragma unroll
-  for (int j = 0; j < PL; ++j) {
-    q[0].e[j] = fsel(prole(j), yq[0], xq[0]);
-    q[1].e[j] = fsel(prole(j), yq[1], xq[1]);
-    S.st6(prole(j), prole(j) ? f6zero() : f6one());
-  }
+  for (int j = 0; j < PL; ++j) S.st6(prole(j), prole(j) ? f6zero() : f6one());
   mp_fence();
 #if defined(__HIP_DEVICE_COMPILE__)
   // the step's two lines staged per wave in LDS (one key per wave), one step ahead
@@ -548,22 +592,28 @@ PV_BN_CALL p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* 
   return mp_get(S);
 }
 
-// bls_check over the pair (both lanes return the verdict)
+// the check over the pair from each lane's coordinates of sigma's and -H(m)'s
+// line points (q[0], q[1]; a point at infinity as 0); both lanes return the verdict
+template <int ST>
+PV_HD bool bls_check_pair_q(pslot<ST> S, const p1 (&q)[2], bool s_inf, bool pk_inf, const uint32_t* g_lines,
+                            const uint32_t* pk_lines) {
+  const bool one = pr_is_one(pr_final_exp(S, miller_pair(S, g_lines, pk_lines, q)));
+  if (s_inf || pk_inf) return s_inf && pk_inf;
+  return one;
+}
+// bls_check's arguments (host checker)
 template <int ST>
 PV_HD bool bls_check_pair(pslot<ST> S, const fp& xs, const fp& ys, bool s_inf, const fp& xqh, const fp& yqh,
                           bool pk_inf, const uint32_t* g_lines, const uint32_t* pk_lines) {
-  fp xq[2], yq[2];
-  if (s_inf) {
-    xq[0] = fzero();
-    yq[0] = fzero();
-  } else {
-    line_point(xs, ys, false, xq[0], yq[0]);
+  fp xq = fzero(), yq = fzero();
+  if (!s_inf) line_point(xs, ys, false, xq, yq);
+  p1 q[2];
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    q[0].e[j] = fsel(prole(j), yq, xq);
+    q[1].e[j] = fsel(prole(j), yqh, xqh);
   }
-  xq[1] = xqh;
-  yq[1] = yqh;
-  const bool one = pr_is_one(pr_final_exp(S, miller_pair(S, g_lines, pk_lines, xq, yq)));
-  if (s_inf || pk_inf) return s_inf && pk_inf;
-  return one;
+  return bls_check_pair_q(S, q, s_inf, pk_inf, g_lines, pk_lines);
 }
 
 }  // namespace bn

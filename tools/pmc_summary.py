@@ -71,7 +71,10 @@ def main(d, units=None):
     if bls_k:
         out['check_kernel'] = bls_k
         if curve_k is None:
-            out['hbm_bytes_per_launch'] = out['kernels'][bls_k].get('hbm_bytes_per_launch')
+            # the lane-pair check kernel and the sigma-prep kernel that feeds it
+            parts = [out['kernels'][k].get('hbm_bytes_per_launch') for k in out['kernels']
+                     if k == bls_k or k.startswith('pvbls::k_bls_sigprep')]
+            out['hbm_bytes_per_launch'] = None if None in parts else sum(parts)
     if units:
         out['units_per_launch'] = units
         if out['hbm_bytes_per_launch'] is not None:
