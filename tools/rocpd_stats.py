@@ -1,40 +1,31 @@
-"""Kernel statistics from a rocprofv3 SQLite output (run_results.db: rocprofv3
-on this image writes rocpd databases by default), in the layout of the
-round-1 --stats summaries: per kernel calls, total / avg / min / max duration.
+"""Kernel statistics from a rocprofv3 --kernel-trace --stats database (rocpd
+SQLite, the image's default output format): per kernel the calls, total and
+average duration, and the average over the dispatches of its LARGEST grid (the
+bench line's launch; the small latency calls of the same run are excluded).
 
-    python tools/rocpd_stats.py DIR_OR_DB [--timeline KERNEL_SUBSTR]
-
---timeline also prints every dispatch of the matching kernel (start, end,
-duration, stream), to read pipelined launches (overlapping intervals)."""
-import glob
-import os
+    python tools/rocpd_stats.py gpurun_out/<dir>/run_results.db > profiles/rNN_..._kernel_stats.txt
+"""
 import sqlite3
 import sys
 
 
-def main():
-    p = sys.argv[1]
-    db = p if p.endswith('.db') else glob.glob(os.path.join(p, '**', '*.db'), recursive=True)[0]
-    cur = sqlite3.connect(db).cursor()
-    rows = cur.execute('select name, count(*), sum(duration), avg(duration), min(duration), max(duration) '
-                       'from kernels group by name order by sum(duration) desc').fetchall()
-    tot = sum(r[2] for r in rows)
-    print('# {}  (durations in us)'.format(db))
-    print('{:<34} {:>6} {:>12} {:>10} {:>10} {:>10} {:>6}'.format('kernel', 'calls', 'total', 'avg', 'min', 'max', '%'))
-    for name, n, s, a, lo, hi in rows:
-        short = name.split('(')[0]
-        print('{:<34} {:>6} {:>12.1f} {:>10.1f} {:>10.1f} {:>10.1f} {:>6.2f}'.format(
-            short[:34], n, s / 1e3, a / 1e3, lo / 1e3, hi / 1e3, 100.0 * s / tot))
-    if '--timeline' in sys.argv:
-        sub = sys.argv[sys.argv.index('--timeline') + 1]
-        ev = cur.execute('select start, end, duration, stream from kernels where name like ? order by start',
-                         ('%' + sub + '%',)).fetchall()
-        if ev:
-            t0 = ev[0][0]
-            print('# dispatches of *{}*: start end duration (us) stream'.format(sub))
-            for s, e, d, st in ev:
-                print('{:12.1f} {:12.1f} {:10.1f} {}'.format((s - t0) / 1e3, (e - t0) / 1e3, d / 1e3, st))
+def main(path):
+    c = sqlite3.connect(path)
+    rows = c.execute('select name, duration, grid_x * grid_y * grid_z from kernels').fetchall()
+    per = {}
+    for name, dur, grid in rows:
+        per.setdefault(name.split('(')[0], []).append((float(dur), int(grid)))
+    total = sum(d for v in per.values() for d, _ in v)
+    print('{:<48} {:>7} {:>12} {:>11} {:>7} {:>14} {:>9}'.format(
+        'kernel', 'calls', 'total_ms', 'avg_ms', 'pct', 'big_grid_avg_ms', 'big_calls'))
+    for name, v in sorted(per.items(), key=lambda kv: -sum(d for d, _ in kv[1])):
+        tot = sum(d for d, _ in v)
+        g = max(x for _, x in v)
+        big = [d for d, x in v if x == g]
+        # rocpd durations are in ns
+        print('{:<48} {:>7} {:>12.3f} {:>11.4f} {:>7.2f} {:>14.4f} {:>9}'.format(
+            name[:48], len(v), tot / 1e6, tot / len(v) / 1e6, 100 * tot / total, sum(big) / len(big) / 1e6, len(big)))
 
 
 if __name__ == '__main__':
-    main()
+    main(sys.argv[1])
