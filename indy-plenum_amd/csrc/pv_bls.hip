@@ -48,6 +48,11 @@ constexpr uint32_t BLS_WAVE_CHECKS = 64;   // checks per wave (= the key segment
 #else
 constexpr uint32_t BLS_WAVE_CHECKS = 32;
 #endif
+// calls of at most this many checks run one check per lane QUAD
+// (k_bls_verify_quad: the two Miller loops on two lane pairs, 16 checks per
+// wave): a lone check's chain is a third shorter, the total work larger
+constexpr uint64_t BLS_QUAD_MAX = 8192;
+constexpr uint32_t BLS_QUAD_CHECKS = 16;
 
 __device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
 #pragma unroll
@@ -77,10 +82,8 @@ __global__ __launch_bounds__(64) void k_bls_lines(const uint8_t* __restrict__ pt
 }
 
 // one lane per distinct message: H(m) and (x/y, 1/y) of -H(m)
-__global__ __launch_bounds__(64) void k_bls_hash(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
-                                                 uint32_t n, uint32_t* __restrict__ tab) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void hash_one(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off, uint32_t i,
+                                         uint32_t* __restrict__ tab) {
   uint32_t d[8];
   pv::sha256_msg(d, blob + off[i], off[i + 1] - off[i], 0, 0);
   fp x, y, xq, yq;
@@ -92,21 +95,26 @@ __global__ __launch_bounds__(64) void k_bls_hash(const uint8_t* __restrict__ blo
   st_fp(t + 2 * NL, xq);
   st_fp(t + 3 * NL, yq);
 }
+__global__ __launch_bounds__(64) void k_bls_hash(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+                                                 uint32_t n, uint32_t* __restrict__ tab) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) hash_one(blob, off, i, tab);
+}
 
-// grouping by key: count, padded segment starts (BLS_WAVE_CHECKS-aligned), scatter
+// grouping by key: count, padded segment starts (aligned to the checks per wave), scatter
 // a check whose key index is out of range is never scheduled: its verdict stays 0
 __global__ void k_bls_count(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys, uint32_t* __restrict__ cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && key_idx[i] < nkeys) atomicAdd(cnt + key_idx[i], 1u);
 }
 
-__global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uint32_t* __restrict__ seg,
+__global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uint32_t pad, uint32_t* __restrict__ seg,
                                uint32_t* __restrict__ total) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint32_t s = 0;
   for (uint32_t j = 0; j < k; ++j) {
     seg[j] = s;
-    s += (cnt[j] + BLS_WAVE_CHECKS - 1) & ~(BLS_WAVE_CHECKS - 1);
+    s += (cnt[j] + pad - 1) & ~(pad - 1);
   }
   *total = s;
 }
@@ -159,10 +167,8 @@ __global__ __launch_bounds__(BLS_BLOCK, 1) void k_bls_verify(
 // check i at prep[w * n + i], w = 0..9 x/y, 10..19 1/y, 20 = 1 if sigma decodes
 // to the point at infinity
 constexpr int SIGPREP_WORDS = 2 * NL + 1;
-__global__ __launch_bounds__(64) void k_bls_sigprep(const uint8_t* __restrict__ sig, uint64_t n,
-                                                    uint32_t* __restrict__ prep) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void sigprep_one(const uint8_t* __restrict__ sig, uint64_t n, uint64_t i,
+                                            uint32_t* __restrict__ prep) {
   fp xs, ys, xq = fzero(), yq = fzero();
   bool inf;
   g1_decode(sig + 128ull * i, xs, ys, inf);
@@ -173,6 +179,25 @@ __global__ __launch_bounds__(64) void k_bls_sigprep(const uint8_t* __restrict__ 
     prep[(NL + w) * n + i] = (uint32_t)yq.l[w];
   }
   prep[2 * NL * n + i] = inf ? 1u : 0u;
+}
+__global__ __launch_bounds__(64) void k_bls_sigprep(const uint8_t* __restrict__ sig, uint64_t n,
+                                                    uint32_t* __restrict__ prep) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) sigprep_one(sig, n, i, prep);
+}
+// small calls: the message hashing (blocks [0, hb)) and sigma's prep (the blocks
+// after) in ONE launch, so that the two chains run side by side
+__global__ __launch_bounds__(64) void k_bls_prep(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+                                                 uint32_t n_msgs, uint32_t hb, uint32_t* __restrict__ tab,
+                                                 const uint8_t* __restrict__ sig, uint64_t n,
+                                                 uint32_t* __restrict__ prep) {
+  if (blockIdx.x < hb) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_msgs) hash_one(blob, off, i, tab);
+  } else {
+    const uint64_t i = (uint64_t)(blockIdx.x - hb) * blockDim.x + threadIdx.x;
+    if (i < n) sigprep_one(sig, n, i, prep);
+  }
 }
 
 // one check per lane PAIR (lanes 2c, 2c + 1), one key per wave (slots of
@@ -208,6 +233,41 @@ __global__ __launch_bounds__(BLS_BLOCK, 2) void k_bls_verify_pair(
   }
   const bool ok = bls_check_pair_q(mp_slot(), q, s_inf, st == 1, g_lines, pk_lines);
   if (live && !h) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
+}
+
+// one check per lane QUAD (lanes 4c .. 4c + 3; small batches): lane pair 0 runs
+// e(sigma, g)'s Miller loop, pair 1 e(-H, pk)'s, each on its own LDS slot; the
+// product and the final exponentiation run on both pairs (bls_check_quad_q).
+// 16 checks per wave, slots of `order` padded to 16 per key.
+__global__ __launch_bounds__(BLS_BLOCK, 2) void k_bls_verify_quad(
+    const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
+    const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint32_t n_msgs,
+    const uint32_t* __restrict__ prep, uint64_t n, uint8_t* __restrict__ verdict) {
+  const uint32_t slot = (blockIdx.x * BLS_BLOCK + threadIdx.x) >> 2;
+  const int h = threadIdx.x & 1, own = (threadIdx.x >> 1) & 1;
+  const uint32_t task0 = __builtin_amdgcn_readfirstlane(slot & ~(BLS_QUAD_CHECKS - 1));
+  if (task0 >= *total) return;
+  const uint32_t j = order[slot];
+  const bool live = j != 0xffffffffu;
+  const uint32_t key = __builtin_amdgcn_readfirstlane(live ? key_idx[j] : 0u);
+  const uint32_t* g_lines = lines;
+  const uint32_t* pk_lines = lines + (uint64_t)KEY_LINE_WORDS * (1 + key);
+  const uint8_t st = kstatus[1 + key];
+  p1 q[2] = {{fzero()}, {fzero()}};   // q[0]: this pair's point (sigma for pair 0, -H for pair 1)
+  bool s_inf = true;
+  const bool msg_ok = live && msg_idx[j] < n_msgs;
+  if (live) {
+    s_inf = prep[2 * NL * n + j] != 0;
+    if (own == 0) {
+#pragma unroll
+      for (int w = 0; w < NL; ++w) q[0].e[0].l[w] = (int32_t)prep[(h * NL + w) * n + j];
+    } else if (st == 0 && msg_ok) {
+      q[0].e[0] = ld_fp(msgtab + (uint64_t)MSG_WORDS * msg_idx[j] + (2 + h) * NL);
+    }
+  }
+  const bool ok = bls_check_quad_q(mp_slot(), q, s_inf, st == 1, g_lines, pk_lines);
+  if (live && (threadIdx.x & 3) == 0) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
 }
 #endif
 
@@ -408,7 +468,13 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   if (!ks.nkeys) return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", d.ord);
   if (n > 0x7fffffffull - 64ull * ks.nkeys) return bfail(PV_EINVAL, "too many checks in one call");
   if (n_msgs > 0xffffffffull) return bfail(PV_EINVAL, "too many messages in one call");
-  const uint64_t slots = ((n + BLS_WAVE_CHECKS - 1) / BLS_WAVE_CHECKS + ks.nkeys) * BLS_WAVE_CHECKS;
+#ifdef PV_BLS_ONE_LANE
+  const uint32_t pad = BLS_WAVE_CHECKS;
+#else
+  const bool quad = n <= BLS_QUAD_MAX;
+  const uint32_t pad = quad ? BLS_QUAD_CHECKS : BLS_WAVE_CHECKS;
+#endif
+  const uint64_t slots = ((n + pad - 1) / pad + ks.nkeys) * pad;
   BLS_HIP(d.msgtab.ensure(n_msgs * MSG_WORDS));
   BLS_HIP(d.cnt.ensure(ks.nkeys));
   BLS_HIP(d.cursor.ensure(ks.nkeys));
@@ -419,6 +485,14 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   BLS_HIP(d.sigprep.ensure(n * SIGPREP_WORDS));
 #endif
   BLS_HIP(hipEventRecord(d.ev[0], s));
+#ifndef PV_BLS_ONE_LANE
+  if (quad) {   // message hashing and sigma's prep in one launch (both timed as "hash")
+    const uint32_t hb = blocks_for(n_msgs, 64);
+    if (n_msgs || n)
+      hipLaunchKernelGGL(k_bls_prep, dim3(hb + blocks_for(n, 64)), dim3(64), 0, s, blob, off, (uint32_t)n_msgs, hb,
+                         d.msgtab.p, sig, n, d.sigprep.p);
+  } else
+#endif
   if (n_msgs) hipLaunchKernelGGL(k_bls_hash, dim3(blocks_for(n_msgs, 64)), dim3(64), 0, s, blob, off, (uint32_t)n_msgs,
                                  d.msgtab.p);
   BLS_HIP(hipGetLastError());
@@ -428,7 +502,7 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   BLS_HIP(hipMemsetAsync(d.cursor.p, 0, ks.nkeys * 4, s));
   BLS_HIP(hipMemsetAsync(d.order.p, 0xff, slots * 4, s));
   hipLaunchKernelGGL(k_bls_count, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, ks.nkeys, d.cnt.p);
-  hipLaunchKernelGGL(k_bls_segments, dim3(1), dim3(64), 0, s, d.cnt.p, ks.nkeys, d.seg.p, d.total.p);
+  hipLaunchKernelGGL(k_bls_segments, dim3(1), dim3(64), 0, s, d.cnt.p, ks.nkeys, pad, d.seg.p, d.total.p);
   hipLaunchKernelGGL(k_bls_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, ks.nkeys, d.seg.p,
                      d.cursor.p, d.order.p);
   BLS_HIP(hipGetLastError());
@@ -437,10 +511,15 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   hipLaunchKernelGGL(k_bls_verify, dim3(blocks_for(slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx, key_idx,
                      d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs, verdict);
 #else
-  if (n) hipLaunchKernelGGL(k_bls_sigprep, dim3(blocks_for(n, 64)), dim3(64), 0, s, sig, n, d.sigprep.p);
-  hipLaunchKernelGGL(k_bls_verify_pair, dim3(blocks_for(2 * slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx,
-                     key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs,
-                     d.sigprep.p, n, verdict);
+  if (n && !quad) hipLaunchKernelGGL(k_bls_sigprep, dim3(blocks_for(n, 64)), dim3(64), 0, s, sig, n, d.sigprep.p);
+  if (quad)
+    hipLaunchKernelGGL(k_bls_verify_quad, dim3(blocks_for(4 * slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx,
+                       key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs,
+                       d.sigprep.p, n, verdict);
+  else
+    hipLaunchKernelGGL(k_bls_verify_pair, dim3(blocks_for(2 * slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx,
+                       key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs,
+                       d.sigprep.p, n, verdict);
 #endif
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[3], s));

@@ -537,7 +537,11 @@ __device__ __forceinline__ pslot<MP_CHECKS> mp_slot() {
 // Inlined into the kernel (one call site): as an out-of-line function its
 // wave-uniform arguments (the line pointers) lived in VGPRs and went through
 // scratch at every step.
-template <int ST>
+// QUAD (the small-batch kernel, one check over four lanes): each lane pair runs
+// ONE pairing's Miller loop -- pair 0 over the generator's lines with sigma's
+// point, pair 1 over the key's lines with -H's -- with its point in q[0]; on the
+// host the caller passes that pairing's lines as g_lines.
+template <int ST, bool QUAD = false>
 PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_lines, const p1 (&q)[2]) {
 #pragma unroll
   for (int j = 0; j < PL; ++j) S.st6(prole(j), prole(j) ? f6zero() : f6one());
@@ -560,7 +564,8 @@ PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_li
     mp_fence();
     __builtin_amdgcn_wave_barrier();
   };
-  auto Lg = [&](int kk) -> const uint32_t* { return mf_lines[wv][kk & 1][0]; };
+  const int own = QUAD ? (int)((threadIdx.x >> 1) & 1) : 0;   // the pair's pairing (QUAD)
+  auto Lg = [&](int kk) -> const uint32_t* { return mf_lines[wv][kk & 1][own]; };
   auto Lp = [&](int kk) -> const uint32_t* { return mf_lines[wv][kk & 1][1]; };
   fetch(0);
   stash(0);
@@ -577,7 +582,7 @@ PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_li
       fetch(k + 1);
       if (!add && i != 63) mp_sqr(S);
       mp_line(S, Lg(k), q[0]);
-      mp_line(S, Lp(k), q[1]);
+      if (!QUAD) mp_line(S, Lp(k), q[1]);
       stash(k + 1);
       ++k;
     }
@@ -586,7 +591,7 @@ PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_li
   for (int j = 0; j < 2; ++j, ++k) {
     fetch(k + 1);
     mp_line(S, Lg(k), q[0]);
-    mp_line(S, Lp(k), q[1]);
+    if (!QUAD) mp_line(S, Lp(k), q[1]);
     stash(k + 1);
   }
   return mp_get(S);
@@ -601,6 +606,37 @@ PV_HD bool bls_check_pair_q(pslot<ST> S, const p1 (&q)[2], bool s_inf, bool pk_i
   if (s_inf || pk_inf) return s_inf && pk_inf;
   return one;
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// the other lane pair's value of the same role (quad_perm [2,3,0,1])
+__device__ __forceinline__ fp qx_fp(const fp& x) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = __builtin_amdgcn_mov_dpp(x.l[i], 0x4E, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ p6 pqswap(const p6& x) {
+  const fp6& c = x.e[0];
+  p6 r;
+  r.e[0] = fp6{fp2{qx_fp(c.c0.a), qx_fp(c.c0.b)}, fp2{qx_fp(c.c1.a), qx_fp(c.c1.b)}, fp2{qx_fp(c.c2.a), qx_fp(c.c2.b)}};
+  return r;
+}
+#endif
+#if defined(__HIPCC__)
+// the check over a lane QUAD (small batches): the two pairs' Miller values are
+// multiplied (each pair forms the same product) and both run the final
+// exponentiation in lockstep; q[0] = the pair's own point coordinate
+__device__ __forceinline__ bool bls_check_quad_q(pslot<MP_CHECKS> S, const p1 (&q)[2], bool s_inf, bool pk_inf,
+                                                 const uint32_t* g_lines, const uint32_t* pk_lines) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const p6 f = miller_pair<MP_CHECKS, true>(S, g_lines, pk_lines, q);
+  const bool one = pr_is_one(pr_final_exp(S, pr_mul(f, pqswap(f))));
+  if (s_inf || pk_inf) return s_inf && pk_inf;
+  return one;
+#else
+  return false;
+#endif
+}
+#endif
 // bls_check's arguments (host checker)
 template <int ST>
 PV_HD bool bls_check_pair(pslot<ST> S, const fp& xs, const fp& ys, bool s_inf, const fp& xqh, const fp& yqh,

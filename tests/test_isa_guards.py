@@ -90,11 +90,12 @@ def test_bls_check_kernel_reads_lines_with_vector_loads(disasm):
         name = disasm[i].split('<')[1].rstrip('>:')
         bodies[name] = disasm[i:fn[k + 1] if k + 1 < len(fn) else len(disasm)]
     verify = [n for n in bodies if 'k_bls_verify' in n]
-    assert len(verify) == 1
-    smem = [ln for ln in bodies[verify[0]] if re.search(r'\ss_load_', ln)]
-    assert smem and len(smem) <= 16, smem
-    assert all(re.search(r's_load_\w+\s+[^,]+,\s+s\[(0:1|[2-9]:\d+|1\d:\d+)\],\s+0x[0-9a-f]+', ln) for ln in smem)
-    assert [ln for ln in bodies[verify[0]] if re.search(r'\s(global|flat)_load_', ln)]
+    assert len(verify) == 2    # the lane-pair and lane-quad check kernels
+    for v in verify:
+        smem = [ln for ln in bodies[v] if re.search(r'\ss_load_', ln)]
+        assert smem and len(smem) <= 16, smem
+        assert all(re.search(r's_load_\w+\s+[^,]+,\s+s\[(0:1|[2-9]:\d+|1\d:\d+)\],\s+0x[0-9a-f]+', ln) for ln in smem)
+        assert [ln for ln in bodies[v] if re.search(r'\s(global|flat)_load_', ln)]
     for n, body in bodies.items():
         if n.startswith('_ZN2bn'):
             assert not [ln for ln in body if re.search(r'\ss_load_', ln)], n

@@ -152,6 +152,38 @@ int bnc_verify_pair(const uint8_t* sig128, const uint8_t* m, uint64_t n, const u
   return bls_check_pair(S, xs, ys, s_inf, xqh, yqh, st == 1, gl, pl) ? 1 : 0;
 }
 
+// ... and on the lane-QUAD kernel's schedule (k_bls_verify_quad: one pairing's
+// Miller loop per lane pair, the pairs' values multiplied, one final exponentiation)
+int bnc_verify_quad(const uint8_t* sig128, const uint8_t* m, uint64_t n, const uint8_t* pk128, const uint8_t* gen128) {
+  static uint32_t gl[N_LINES * LINE_WORDS], pl[N_LINES * LINE_WORDS];
+  if (bnc_g2_lines(gen128, gl) != 0) return -1;
+  g2a q;
+  const int st = g2_decode(pk128, q);
+  if (st == 0) g2_lines(pl, q);
+  else memset(pl, 0, sizeof pl);
+  uint8_t h[128];
+  bnc_hash_to_g1(m, n, h);
+  const fp hx = to_mont(from_be32(h + 1)), hy = to_mont(from_be32(h + 33));
+  fp xqh, yqh;
+  line_point(hx, hy, true, xqh, yqh);
+  if (st != 0) xqh = yqh = fzero();
+  fp xs, ys, xq = fzero(), yq = fzero();
+  bool s_inf;
+  g1_decode(sig128, xs, ys, s_inf);
+  if (!s_inf) line_point(xs, ys, false, xq, yq);
+  p1 qa[2], qb[2];
+  for (int j = 0; j < PL; ++j) {
+    qa[0].e[j] = qa[1].e[j] = fsel(prole(j), yq, xq);
+    qb[0].e[j] = qb[1].e[j] = fsel(prole(j), yqh, xqh);
+  }
+  uint32_t sa[12 * NL], sb[12 * NL];
+  const p6 fa = miller_pair<1, true>(pslot<1>{sa}, gl, nullptr, qa);
+  const p6 fb = miller_pair<1, true>(pslot<1>{sb}, pl, nullptr, qb);
+  const bool one = pr_is_one(pr_final_exp(pslot<1>{sa}, pr_mul(fa, fb)));
+  if (s_inf || st == 1) return (s_inf && st == 1) ? 1 : 0;
+  return one ? 1 : 0;
+}
+
 // the Fp multiplies / squarings of ONE check as k_bls_verify runs it (sigma
 // decoding + bls_check; the lines and H(m) are per key / per message and are
 // prepared before the counters are reset): out = {mul, sqr}
