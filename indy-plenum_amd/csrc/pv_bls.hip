@@ -51,7 +51,10 @@ constexpr uint32_t BLS_WAVE_CHECKS = 32;
 // calls of at most this many checks run one check per lane QUAD
 // (k_bls_verify_quad: the two Miller loops on two lane pairs, 16 checks per
 // wave): a lone check's chain is a third shorter, the total work larger
-constexpr uint64_t BLS_QUAD_MAX = 8192;
+#ifndef PV_BLS_QUAD_MAX
+#define PV_BLS_QUAD_MAX 8192
+#endif
+constexpr uint64_t BLS_QUAD_MAX = PV_BLS_QUAD_MAX;
 constexpr uint32_t BLS_QUAD_CHECKS = 16;
 
 __device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
