@@ -68,9 +68,10 @@ W_SQ_PER_VERIFY = 1022.0
 W_MAD_PER_VERIFY = int(W_MUL_PER_VERIFY * 100 + W_SQ_PER_VERIFY * 55)
 W_MUL_FULL, W_SQ_FULL = 1587.5, 1517.0
 W_MAD_FULL = int(W_MUL_FULL * 100 + W_SQ_FULL * 55)
-# curve_mode PV_CURVE_GROUPED: full-length scalars, CURVE_K = 4 signatures per lane
-# sharing one inversion (3 of every 4 254-squaring inversions become 3 multiplies)
-W_MUL_GROUPED, W_SQ_GROUPED = 1581.5, 1326.5
+# curve_mode PV_CURVE_GROUPED: full-length scalars, CURVE_K = 8 signatures per lane
+# sharing one inversion (7 of every 8 254-squaring inversions become 3 multiplies;
+# the keyed kernels below share theirs the same way)
+W_MUL_GROUPED, W_SQ_GROUPED = 1580.5, 1294.75
 W_MAD_GROUPED = int(W_MUL_GROUPED * 100 + W_SQ_GROUPED * 55)
 # keyed batches (prepared keys, 8-way comb of -A over the 32-bit words of h):
 # 28 doublings instead of 253, no decompression; decompression and the comb
@@ -78,7 +79,7 @@ W_MAD_GROUPED = int(W_MUL_GROUPED * 100 + W_SQ_GROUPED * 55)
 # per distinct key in k_keys
 # (base-point digits in radix 2^16 from the eight chunk tables k * 2^(32 q) * B:
 # 16 affine adds instead of 32, 762 -> 650 multiplies per verify)
-W_MUL_KEYED, W_SQ_KEYED = 650.0, 175.5
+W_MUL_KEYED, W_SQ_KEYED = 649.0, 143.75
 W_MUL_KEYPREP, W_SQ_KEYPREP = 1547.5, 1321.0
 W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
 # wide key format (radix-256 comb, --key-format wide; C3's node keys by default):
@@ -86,7 +87,7 @@ W_MAD_KEYED = int(W_MUL_KEYED * 100 + W_SQ_KEYED * 55)
 # built by 128 lanes that each redo the decode and A_q's doublings (latency over
 # work: 7.3x the one-lane-per-table work per key, 1.2 -> ~0.7 ms for 25 keys)
 # (host op counts, tests/test_hostcheck.py::test_keyed_wide_raw_vectors_and_op_counts)
-W_MUL_KEYED_WIDE, W_SQ_KEYED_WIDE = 414.0, 159.5
+W_MUL_KEYED_WIDE, W_SQ_KEYED_WIDE = 413.0, 127.75
 W_MUL_KEYPREP_WIDE, W_SQ_KEYPREP_WIDE = 69940.0, 126080.0
 W_MAD_KEYED_WIDE = int(W_MUL_KEYED_WIDE * 100 + W_SQ_KEYED_WIDE * 55)
 # v_mad_u64_u32 issue ceiling of one MI355X measured by tools/ubench/mad_peak.hip

@@ -299,7 +299,7 @@ int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *
  *                       the ~0.2 % of signatures whose h has no such (c, d) get the
  *                       full-length verdict in the same launch;
  *     PV_CURVE_FULL     every signature through the full-length verdict;
- *     PV_CURVE_GROUPED  the full-length kernel, 4 signatures per lane sharing one
+ *     PV_CURVE_GROUPED  the full-length kernel, 8 signatures per lane sharing one
  *                       inversion.
  *   lat_max         generic batches of at most this many signatures (per device
  *                   call / host-buffer shard) run the latency kernel: 8 lanes per

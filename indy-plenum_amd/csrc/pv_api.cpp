@@ -341,7 +341,7 @@ KeyCache g_kc;
 // PV_CURVE_MODE (read at pv_init): "half" (default) = half-size scalars with
 // full-length tasks for deferred records; "full" = every record deferred
 // (full-length verdicts through the same kernel: A/B timing and tests);
-// "grouped" = the previous generic kernel (k_curve, 4 signatures per lane
+// "grouped" = the previous generic kernel (k_curve, 8 signatures per lane
 // sharing one inversion).  Verdicts are identical in every mode.
 enum class CurveMode { Half, Full, Grouped };
 

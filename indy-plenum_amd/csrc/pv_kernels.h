@@ -13,7 +13,10 @@ constexpr int BTAB_WORDS = 32;
 constexpr int BTAB_CHUNKS = 8;     // tables for 2^(32 q) B, q = 0..7 (comb kernel of prepared keys)
 // per-lane scratch: A table (9 cached entries k*(-A), 40 words each) + the
 // CURVE_K points awaiting the shared inversion (40 words each)
-constexpr int ATAB_WORDS = 9 * 40 + 4 * 40;
+#ifndef PV_CURVE_K
+#define PV_CURVE_K 8
+#endif
+constexpr int ATAB_WORDS = 9 * 40 + PV_CURVE_K * 40;
 constexpr int CURVE_BLOCK = 256;
 constexpr int HASH_BLOCK = 256;
 

@@ -1068,7 +1068,10 @@ PV_HD bool curve_point_keyed(ge_p2& rp, const uint32_t* kt, const uint8_t* sig, 
 // Signatures one lane finishes together: their final Z^-1 share ONE field
 // inversion (Montgomery's trick: 3(K-1) multiplies + 1 inversion instead of
 // K inversions).
-constexpr int CURVE_K = 4;
+#ifndef PV_CURVE_K
+#define PV_CURVE_K 8
+#endif
+constexpr int CURVE_K = PV_CURVE_K;
 constexpr int PT_WORDS = 40;                        // X, Y, Z, prefix product
 constexpr int LANE_WORDS = AT_WORDS + CURVE_K * PT_WORDS;
 

@@ -196,7 +196,7 @@ def test_op_counts_pin_valu_constants(hc):
 
 
 def test_op_counts_pin_grouped_constants(hc):
-    """curve_mode PV_CURVE_GROUPED: groups of CURVE_K = 4 signatures share the final inversion."""
+    """curve_mode PV_CURVE_GROUPED: groups of CURVE_K = 8 signatures share the final inversion."""
     import bench
     n = 16
     pk, sig, blob, off = _signed_batch(n, 4)
