@@ -188,15 +188,81 @@ __global__ __launch_bounds__(64) void k_bls_sigprep(const uint8_t* __restrict__ 
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) sigprep_one(sig, n, i, prep);
 }
-// small calls: the message hashing (blocks [0, hb)) and sigma's prep (the blocks
-// after) in ONE launch, so that the two chains run side by side
+// a^(r ? E_ISQRT : E_SQRT) with the loop's branches uniform over a lane group
+// whose lanes hold both r: a multiply runs where either exponent has a bit (67
+// of 253 bits) and only lanes whose own exponent has it keep the product
+__device__ __forceinline__ fp pow_root_pair(const fp& a, int r) {
+  fp acc = fone(), b = a;
+  for (int w = 0; w < 4; ++w) {
+    const uint64_t es = E_SQRT[w], ei = E_ISQRT[w];
+    for (int k = 0; k < 64; ++k) {
+      const bool bs = (es >> k) & 1, bi = (ei >> k) & 1;
+      if (bs || bi) {
+        const fp t = mul(acc, b);
+        if (r ? bi : bs) acc = t;
+      }
+      if (w < 3 || ((es | ei) >> k) > 1) b = sqr(b);
+    }
+  }
+  return acc;
+}
+__device__ __forceinline__ fp shfl_fp(const fp& x, int src) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = __shfl(x.l[i], src);
+  return r;
+}
+
+// small calls: H(m) over a group of 8 lanes per message.  Lane (c, r) = (lg >> 1,
+// lg & 1) takes candidate xi + c (+ 4 per round) of hash_to_g1's increment map
+// and forms, side by side, y = a^((p+1)/4) (r = 0) and a^((3p-5)/4) (r = 1; = 1/y
+// when a = x^3 + 2 is a non-zero square, since the two exponents sum to p - 1):
+// the lowest candidate whose a is a non-zero square is hash_to_g1's point (the
+// same increment order), and -H's line point (x/y, 1/y) takes no inversion.  The
+// serial hash_one runs ~2 square roots and an inversion one after another; this
+// chain is one exponentiation.  Control flow is uniform over a group.
+__device__ __forceinline__ void hash_group(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+                                           uint32_t i, uint32_t* __restrict__ tab) {
+  const int lane = threadIdx.x & 63, lg = lane & 7, base = lane & ~7, r = lg & 1;
+  uint32_t d[8];
+  pv::sha256_msg(d, blob + off[i], off[i + 1] - off[i], 0, 0);
+  fp xi = from_be32(reinterpret_cast<const uint8_t*>(d));
+  xi.l[0] += lg >> 1;
+  xi = norm(xi);
+  for (;;) {
+    const fp x = to_mont(xi);
+    const fp a = addn(mul(sqr(x), x), cst(TWO_M));
+    const fp e = pow_root_pair(a, r);
+    const fp o = shfl_fp(e, lane ^ 1);
+    const fp y = r ? o : e, yi = r ? e : o;
+    const bool ok = eq(sqr(y), a) && !is_zero(a);
+    const uint32_t gm = (uint32_t)(__ballot(ok) >> base) & 0xffu;
+    if (gm) {
+      if (lg == __builtin_ctz(gm)) {   // the winning candidate's r = 0 lane
+        const fp yq = negn(yi), xq = mul(x, yq);
+        uint32_t* t = tab + (uint64_t)MSG_WORDS * i;
+        st_fp(t, x);
+        st_fp(t + NL, y);
+        st_fp(t + 2 * NL, xq);
+        st_fp(t + 3 * NL, yq);
+      }
+      return;
+    }
+    xi.l[0] += 4;
+    xi = norm(xi);
+  }
+}
+
+// small calls: the message hashing (blocks [0, hb), 8 lanes per message) and
+// sigma's prep (the blocks after, one lane per check) in ONE launch, so that the
+// two chains run side by side
 __global__ __launch_bounds__(64) void k_bls_prep(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
                                                  uint32_t n_msgs, uint32_t hb, uint32_t* __restrict__ tab,
                                                  const uint8_t* __restrict__ sig, uint64_t n,
                                                  uint32_t* __restrict__ prep) {
   if (blockIdx.x < hb) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n_msgs) hash_one(blob, off, i, tab);
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+    if (i < n_msgs) hash_group(blob, off, (uint32_t)i, tab);
   } else {
     const uint64_t i = (uint64_t)(blockIdx.x - hb) * blockDim.x + threadIdx.x;
     if (i < n) sigprep_one(sig, n, i, prep);
@@ -490,7 +556,7 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   BLS_HIP(hipEventRecord(d.ev[0], s));
 #ifndef PV_BLS_ONE_LANE
   if (quad) {   // message hashing and sigma's prep in one launch (both timed as "hash")
-    const uint32_t hb = blocks_for(n_msgs, 64);
+    const uint32_t hb = blocks_for(8 * n_msgs, 64);
     if (n_msgs || n)
       hipLaunchKernelGGL(k_bls_prep, dim3(hb + blocks_for(n, 64)), dim3(64), 0, s, blob, off, (uint32_t)n_msgs, hb,
                          d.msgtab.p, sig, n, d.sigprep.p);

@@ -366,23 +366,9 @@ PV_HD p6 mp_get(pslot<ST> S) {
 // (x.a + x.b)(y.a + y.b) is split at the Fp2 level -- role 0 forms its v0, v1,
 // v2, role 1 its s12, s01, s02.  Role 0 writes t0 + v t1, role 1 s - t0 - t1:
 // the same sums as f12mul, so the same limbs.
-PV_BN_CALL p6 pr_mul(const p6& x, const p6& y) {
-  p6 t;   // the out-of-line product first: nothing else is live across the call
-#pragma unroll
-  for (int j = 0; j < PL; ++j) t.e[j] = f6mul(x.e[j], y.e[j]);
-  p2 m[3];
-  {
-    const p6 xo = pswap(x), yo = pswap(y);
-#pragma unroll
-    for (int j = 0; j < PL; ++j) {
-      const int h = prole(j);
-      const fp6 X = f6add(x.e[j], xo.e[j]), Y = f6add(y.e[j], yo.e[j]);
-      // role 0: X_k Y_k (k = 0, 1, 2); role 1: (X_a + X_b)(Y_a + Y_b) for (a, b) = (1, 2), (0, 1), (0, 2)
-      m[0].e[j] = f2mul(f2sel(h, f2addL(X.c1, X.c2), X.c0), f2sel(h, f2add(Y.c1, Y.c2), Y.c0));
-      m[1].e[j] = f2mul(f2sel(h, f2addL(X.c0, X.c1), X.c1), f2sel(h, f2add(Y.c0, Y.c1), Y.c1));
-      m[2].e[j] = f2mul(f2sel(h, f2addL(X.c0, X.c2), X.c2), f2sel(h, f2add(Y.c0, Y.c2), Y.c2));
-    }
-  }
+// the sums of pr_mul from the lane's own-half product t and the three Fp2
+// products m of s (role 0 v0, v1, v2; role 1 s12, s01, s02)
+PV_HD p6 pr_mul_tail(const p6& t, const p2 (&m)[3]) {
   const p6 to = pswap(t);
   const p2 mo[3] = {pswap(m[0]), pswap(m[1]), pswap(m[2])};
   p6 r;
@@ -403,6 +389,25 @@ PV_BN_CALL p6 pr_mul(const p6& x, const p6& y) {
     r.e[j] = f6sel(h, rb, ra);
   }
   return r;
+}
+PV_BN_CALL p6 pr_mul(const p6& x, const p6& y) {
+  p6 t;   // the out-of-line product first: nothing else is live across the call
+#pragma unroll
+  for (int j = 0; j < PL; ++j) t.e[j] = f6mul(x.e[j], y.e[j]);
+  p2 m[3];
+  {
+    const p6 xo = pswap(x), yo = pswap(y);
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int h = prole(j);
+      const fp6 X = f6add(x.e[j], xo.e[j]), Y = f6add(y.e[j], yo.e[j]);
+      // role 0: X_k Y_k (k = 0, 1, 2); role 1: (X_a + X_b)(Y_a + Y_b) for (a, b) = (1, 2), (0, 1), (0, 2)
+      m[0].e[j] = f2mul(f2sel(h, f2addL(X.c1, X.c2), X.c0), f2sel(h, f2add(Y.c1, Y.c2), Y.c0));
+      m[1].e[j] = f2mul(f2sel(h, f2addL(X.c0, X.c1), X.c1), f2sel(h, f2add(Y.c0, Y.c1), Y.c1));
+      m[2].e[j] = f2mul(f2sel(h, f2addL(X.c0, X.c2), X.c2), f2sel(h, f2add(Y.c0, Y.c2), Y.c2));
+    }
+  }
+  return pr_mul_tail(t, m);
 }
 PV_HD p6 pr_conj(const p6& x) {
   p6 r;
@@ -476,49 +481,208 @@ PV_HD bool pr_is_one(const p6& x) {
   return pand(ok);
 }
 
-// x^u in the cyclotomic subgroup (cyc_pow_u's chain) with the power in the slot
+// ------------------------------------------------------------------ lane-QUAD final exponentiation
+// In k_bls_verify_quad the two lane pairs of a check (qrole g = 0 / 1) hold the
+// SAME Fp12 halves after the Miller product -- bit-identical, since both pairs
+// form the same sums of the same products -- and split the Fp2 products of each
+// final-exponentiation step between them, exchanging results with quad_perm
+// [2,3,0,1] DPP moves:
+//   an Fp6 product (f6mul_q): g = 0 forms the diagonal v0, v1, v2, g = 1 the
+//   three Karatsuba sums s12, s01, s02 -- 3 products in sequence instead of 6;
+//   an Fp12 product (pr_mul_q): that split for the lane's half product t, m0 of
+//   the third product on g = 0, m1 on g = 1, m2 on both -- 5 instead of 9;
+//   a cyclotomic squaring (mq_cyc_sqr): the Fp4 squaring k = g, then k = 2 on
+//   both pairs -- 2 instead of 3 -- on the quad's shared LDS slot (the even
+//   pair's), each pair writing its own k's coefficients and g = 0 those of k = 2.
+// Every sum is the pair version's (the same integers, so the same limbs).  The
+// host build has no quad: there pmul / pcyc / preduce / pinv are the pair ops.
+#if defined(__HIP_DEVICE_COMPILE__)
+// the other lane pair's value of the same role (quad_perm [2,3,0,1])
+__device__ __forceinline__ fp qx_fp(const fp& x) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = __builtin_amdgcn_mov_dpp(x.l[i], 0x4E, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ fp2 qx_fp2(const fp2& x) { return fp2{qx_fp(x.a), qx_fp(x.b)}; }
+__device__ __forceinline__ p6 pqswap(const p6& x) {
+  const fp6& c = x.e[0];
+  p6 r;
+  r.e[0] = fp6{qx_fp2(c.c0), qx_fp2(c.c1), qx_fp2(c.c2)};
+  return r;
+}
+__device__ __forceinline__ bool qrole() { return (threadIdx.x >> 1) & 1; }
+
+// f6mul_i(x, y) with its six Fp2 products split over the two pairs
+__device__ __forceinline__ fp6 f6mul_q(const fp6& x, const fp6& y) {
+  const bool g = qrole();
+  const fp2 p0 = pin(f2mul(f2sel(g, f2addL(x.c1, x.c2), x.c0), f2sel(g, f2add(y.c1, y.c2), y.c0)));
+  const fp2 p1 = pin(f2mul(f2sel(g, f2addL(x.c0, x.c1), x.c1), f2sel(g, f2add(y.c0, y.c1), y.c1)));
+  const fp2 p2 = pin(f2mul(f2sel(g, f2addL(x.c0, x.c2), x.c2), f2sel(g, f2add(y.c0, y.c2), y.c2)));
+  const fp2 o0 = qx_fp2(p0), o1 = qx_fp2(p1), o2 = qx_fp2(p2);
+  const fp2 v0 = f2sel(g, o0, p0), v1 = f2sel(g, o1, p1), v2 = f2sel(g, o2, p2);
+  const fp2 s12 = f2sel(g, p0, o0), s01 = f2sel(g, p1, o1), s02 = f2sel(g, p2, o2);
+  fp6 r;
+  r.c0 = f2norm(f2addL(f2mulxiL(f2subL(f2subL(s12, v1), v2)), v0));
+  r.c1 = f2norm(f2addL(f2subL(f2subL(s01, v0), v1), f2mulxiL(v2)));
+  r.c2 = f2norm(f2addL(f2subL(f2subL(s02, v0), v2), v1));
+  return r;
+}
+__device__ __noinline__ p6 pr_mul_q(const p6& x, const p6& y) {
+  const int h = prole(0);
+  const bool g = qrole();
+  p6 t;
+  t.e[0] = f6mul_q(x.e[0], y.e[0]);
+  p2 m[3];
+  {
+    const p6 xo = pswap(x), yo = pswap(y);
+    const fp6 X = f6add(x.e[0], xo.e[0]), Y = f6add(y.e[0], yo.e[0]);
+    const fp2 a0 = f2sel(h, f2addL(X.c1, X.c2), X.c0), b0 = f2sel(h, f2add(Y.c1, Y.c2), Y.c0);
+    const fp2 a1 = f2sel(h, f2addL(X.c0, X.c1), X.c1), b1 = f2sel(h, f2add(Y.c0, Y.c1), Y.c1);
+    const fp2 ma = pin(f2mul(f2sel(g, a1, a0), f2sel(g, b1, b0)));   // m0 (g = 0) / m1 (g = 1)
+    m[2].e[0] = pin(f2mul(f2sel(h, f2addL(X.c0, X.c2), X.c2), f2sel(h, f2add(Y.c0, Y.c2), Y.c2)));
+    const fp2 mo = qx_fp2(ma);
+    m[0].e[0] = f2sel(g, mo, ma);
+    m[1].e[0] = f2sel(g, ma, mo);
+  }
+  return pr_mul_tail(t, m);
+}
+// pr_inv with its two Fp6 products split (the Fp6 inverse runs on both pairs)
+__device__ __noinline__ p6 pr_inv_q(const p6& x) {
+  p6 sq;
+  sq.e[0] = f6mul_q(x.e[0], x.e[0]);
+  const p6 so = pswap(sq);
+  const int h = prole(0);
+  const fp6 d = f6inv(f6sub(f6sel(h, so.e[0], sq.e[0]), f6mulv(f6sel(h, sq.e[0], so.e[0]))));
+  const fp6 m = f6mul_q(x.e[0], d);
+  p6 r;
+  r.e[0] = f6sel(h, f6neg(m), m);
+  return r;
+}
+// mp_cyc_sqr over the quad's shared slot: Fp4 squarings k = g and k = 2.  Every
+// read of the slot precedes every write (the pairs read coefficients the other
+// pair writes).
 template <int ST>
+__device__ __forceinline__ void mq_cyc_sqr(pslot<ST> S) {
+  const int h = prole(0);
+  const bool g = qrole();
+  // Z0 = {0, 3, 1}, Z1 = {4, 2, 5}; outputs O0 = {0, 1, 2} (role 0), O1 = {4, 5, 3} (role 1)
+  fp2 pa, p2v;
+  {
+    const fp2 z0 = S.ld(g ? 3 : 0), z1 = S.ld(g ? 2 : 4);
+    pa = pin(f2mul(f2sel(h, z0, f2addL(z0, z1)), f2sel(h, z1, f2norm(f2addL(f2mulxiL(z1), z0)))));
+  }
+  mp_fence();
+  {
+    const fp2 z0 = S.ld(1), z1 = S.ld(5);
+    p2v = pin(f2mul(f2sel(h, z0, f2addL(z0, z1)), f2sel(h, z1, f2norm(f2addL(f2mulxiL(z1), z0)))));
+  }
+  const int ea = h ? (g ? 5 : 4) : (g ? 1 : 0), e2 = h ? 3 : 2;
+  const fp2 za = S.ld(ea), z2 = S.ld(e2);
+  mp_fence();
+  fp2 outa, out2;
+  {
+    const fp2 q = px_fp2(pa);
+    const fp2 u = f2norm(f2subL(f2subL(pa, f2sel(h, f2negL(pa), q)), f2sel(h, f2zero(), f2mulxiL(q))));
+    const fp2 zs = f2sel(h, za, f2negL(za));
+    outa = f2norm(f2addL(f2addL(f2addL(u, u), u), f2addL(zs, zs)));
+  }
+  {
+    const fp2 q = px_fp2(p2v);
+    const fp2 a = f2sel(h, f2mulxiL(p2v), p2v);
+    const fp2 u = f2norm(f2subL(f2subL(a, f2sel(h, f2negL(a), q)), f2sel(h, f2zero(), f2mulxiL(q))));
+    const fp2 zs = f2sel(h, z2, f2negL(z2));
+    out2 = f2norm(f2addL(f2addL(f2addL(u, u), u), f2addL(zs, zs)));
+  }
+  S.st(ea, outa);
+  if (!g) S.st(e2, out2);
+  mp_fence();
+}
+// mp_reduce over the quad: components g and 2 of the lane's half
+template <int ST>
+__device__ __forceinline__ void mq_reduce(pslot<ST> S) {
+  const int h = prole(0);
+  const bool g = qrole();
+  const int ea = 3 * h + (int)g, e2 = 3 * h + 2;
+  const fp2 ra = f2reduce(S.ld(ea)), r2 = f2reduce(S.ld(e2));
+  mp_fence();
+  S.st(ea, ra);
+  if (!g) S.st(e2, r2);
+  mp_fence();
+}
+#endif
+template <bool Q>
+PV_HD p6 pmul(const p6& x, const p6& y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (Q) return pr_mul_q(x, y);
+#endif
+  return pr_mul(x, y);
+}
+template <bool Q>
+PV_HD p6 pinv(const p6& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (Q) return pr_inv_q(x);
+#endif
+  return pr_inv(x);
+}
+template <bool Q, int ST>
+PV_HD void pcyc(pslot<ST> S) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (Q) return mq_cyc_sqr(S);
+#endif
+  mp_cyc_sqr(S);
+}
+template <bool Q, int ST>
+PV_HD void preduce(pslot<ST> S) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (Q) return mq_reduce(S);
+#endif
+  mp_reduce(S);
+}
+
+// x^u in the cyclotomic subgroup (cyc_pow_u's chain) with the power in the slot
+template <int ST, bool Q = false>
 PV_BN_CALL p6 pr_pow_u(pslot<ST> S, const p6& x) {
   mp_put(S, x);
   for (int i = 0; i < 7; ++i) {
-    mp_cyc_sqr(S);
-    if ((i & 3) == 3) mp_reduce(S);
+    pcyc<Q>(S);
+    if ((i & 3) == 3) preduce<Q>(S);
   }
-  mp_put(S, pr_mul(mp_get(S), x));   // x^(2^7 + 1)
+  mp_put(S, pmul<Q>(mp_get(S), x));   // x^(2^7 + 1)
   for (int i = 0; i < 55; ++i) {
-    mp_cyc_sqr(S);
-    if ((i & 3) == 3) mp_reduce(S);
+    pcyc<Q>(S);
+    if ((i & 3) == 3) preduce<Q>(S);
   }
-  return pr_conj(pr_mul(mp_get(S), x));   // x^(2^62 + 2^55 + 1), conjugated
+  return pr_conj(pmul<Q>(mp_get(S), x));   // x^(2^62 + 2^55 + 1), conjugated
 }
-template <int ST>
+template <int ST, bool Q = false>
 PV_BN_CALL p6 pr_cyc_sqr(pslot<ST> S, const p6& x) {
   mp_put(S, x);
-  mp_cyc_sqr(S);
+  pcyc<Q>(S);
   return mp_get(S);
 }
 
 // final_exp's chain on halves
-template <int ST>
+template <int ST, bool Q = false>
 PV_BN_CALL p6 pr_final_exp(pslot<ST> S, const p6& f0) {
-  p6 f = pr_mul(pr_conj(f0), pr_inv(f0));   // ^(p^6 - 1)
-  f = pr_mul(pr_frob2(f), f);              // ^(p^2 + 1)
-  const p6 fu = pr_pow_u(S, f);
-  const p6 fu2 = pr_pow_u(S, fu);
-  const p6 fu3 = pr_pow_u(S, fu2);
-  const p6 y6 = pr_conj(pr_mul(fu3, pr_frob1(fu3)));
-  p6 t0 = pr_cyc_sqr(S, y6);
-  t0 = pr_mul(t0, pr_conj(pr_mul(fu, pr_frob1(fu2))));   // y4
+  p6 f = pmul<Q>(pr_conj(f0), pinv<Q>(f0));   // ^(p^6 - 1)
+  f = pmul<Q>(pr_frob2(f), f);              // ^(p^2 + 1)
+  const p6 fu = pr_pow_u<ST, Q>(S, f);
+  const p6 fu2 = pr_pow_u<ST, Q>(S, fu);
+  const p6 fu3 = pr_pow_u<ST, Q>(S, fu2);
+  const p6 y6 = pr_conj(pmul<Q>(fu3, pr_frob1(fu3)));
+  p6 t0 = pr_cyc_sqr<ST, Q>(S, y6);
+  t0 = pmul<Q>(t0, pr_conj(pmul<Q>(fu, pr_frob1(fu2))));   // y4
   const p6 y5 = pr_conj(fu2);
-  t0 = pr_mul(t0, y5);
-  p6 t1 = pr_mul(pr_mul(pr_conj(pr_frob1(fu)), y5), t0);
-  t0 = pr_mul(t0, pr_frob2(fu2));
-  t1 = pr_mul(pr_cyc_sqr(S, t1), t0);
-  t1 = pr_cyc_sqr(S, t1);
-  t0 = pr_mul(t1, pr_conj(f));
-  const p6 y0 = pr_mul(pr_mul(pr_frob1(f), pr_frob2(f)), pr_frob3(f));
-  t1 = pr_mul(t1, y0);
-  return pr_mul(pr_cyc_sqr(S, t0), t1);
+  t0 = pmul<Q>(t0, y5);
+  p6 t1 = pmul<Q>(pmul<Q>(pr_conj(pr_frob1(fu)), y5), t0);
+  t0 = pmul<Q>(t0, pr_frob2(fu2));
+  t1 = pmul<Q>(pr_cyc_sqr<ST, Q>(S, t1), t0);
+  t1 = pr_cyc_sqr<ST, Q>(S, t1);
+  t0 = pmul<Q>(t1, pr_conj(f));
+  const p6 y0 = pmul<Q>(pmul<Q>(pr_frob1(f), pr_frob2(f)), pr_frob3(f));
+  t1 = pmul<Q>(t1, y0);
+  return pmul<Q>(pr_cyc_sqr<ST, Q>(S, t0), t1);
 }
 
 #if defined(__HIPCC__)
@@ -606,21 +770,6 @@ PV_HD bool bls_check_pair_q(pslot<ST> S, const p1 (&q)[2], bool s_inf, bool pk_i
   if (s_inf || pk_inf) return s_inf && pk_inf;
   return one;
 }
-#if defined(__HIP_DEVICE_COMPILE__)
-// the other lane pair's value of the same role (quad_perm [2,3,0,1])
-__device__ __forceinline__ fp qx_fp(const fp& x) {
-  fp r;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) r.l[i] = __builtin_amdgcn_mov_dpp(x.l[i], 0x4E, 0xf, 0xf, false);
-  return r;
-}
-__device__ __forceinline__ p6 pqswap(const p6& x) {
-  const fp6& c = x.e[0];
-  p6 r;
-  r.e[0] = fp6{fp2{qx_fp(c.c0.a), qx_fp(c.c0.b)}, fp2{qx_fp(c.c1.a), qx_fp(c.c1.b)}, fp2{qx_fp(c.c2.a), qx_fp(c.c2.b)}};
-  return r;
-}
-#endif
 #if defined(__HIPCC__)
 // the check over a lane QUAD (small batches): the two pairs' Miller values are
 // multiplied (each pair forms the same product) and both run the final
@@ -629,7 +778,13 @@ __device__ __forceinline__ bool bls_check_quad_q(pslot<MP_CHECKS> S, const p1 (&
                                                  const uint32_t* g_lines, const uint32_t* pk_lines) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const p6 f = miller_pair<MP_CHECKS, true>(S, g_lines, pk_lines, q);
-  const bool one = pr_is_one(pr_final_exp(S, pr_mul(f, pqswap(f))));
+  // both pairs multiply sigma's value (pair 0's) by -H's (pair 1's) in that order,
+  // so that both hold the same limbs from here on
+  const p6 o = pqswap(f);
+  const bool g = qrole();
+  const p6 fs = g ? o : f, fh = g ? f : o;
+  const pslot<MP_CHECKS> Sq{S.c & ~1u};   // the even pair's slot, shared by the quad
+  const bool one = pr_is_one(pr_final_exp<MP_CHECKS, true>(Sq, pr_mul_q(fs, fh)));
   if (s_inf || pk_inf) return s_inf && pk_inf;
   return one;
 #else
