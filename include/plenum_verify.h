@@ -331,6 +331,9 @@ int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *
  *                   first_pct 50 (10..100), copy threads 8 (1..64), pin 512 MB
  *                   (16..4096).
  *   host_trace      1 = per-chunk host timings of pv_verify_batch on stderr.
+ *   bls_quad_max    BLS calls (pv_bls_verify_*) of at most this many checks run
+ *                   one check per lane quad (latency), larger ones one per lane
+ *                   pair (throughput).  Default 32768 (0..2^20).
  *   test_dup_devices  TEST ONLY, read by the next pv_init: 2..8 opens that many
  *                   engine devices, all on HIP device 0, so the multi-device
  *                   paths (a worker thread per device, shard offsets, error
@@ -364,7 +367,7 @@ typedef struct pv_tuning {
   uint32_t host_pin_max_mb;
   uint32_t host_trace;
   uint32_t test_dup_devices;
-  uint32_t reserved;
+  uint32_t bls_quad_max;
 } pv_tuning;
 int pv_get_tuning(pv_tuning *t);
 int pv_set_tuning(const pv_tuning *t);

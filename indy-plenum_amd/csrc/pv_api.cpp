@@ -29,6 +29,10 @@
 static_assert(PV_KEY_WORDS == (unsigned)pv::KEYTAB_WORDS, "prepared-key layout");
 static_assert(PV_KEY_WORDS_WIDE == (unsigned)pv::KEYTAB_WIDE_WORDS, "wide prepared-key layout");
 
+namespace pvbls {
+void set_quad_max(uint64_t n);   // pv_bls.hip
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -58,6 +62,9 @@ int fail(int code, const char* fmt, ...) {
 // keyed batches (prepared keys) of at most this many signatures run the keyed
 // latency kernel (k_verify_quad_keyed); tuning.lat_keyed_max (0 disables)
 #define PV_LAT_KEYED_MAX 8192
+// BLS calls of at most this many checks run the lane-quad check kernel
+// (pv_bls.hip; the same default as its PV_BLS_QUAD_MAX); tuning.bls_quad_max
+#define PV_BLS_QUAD_MAX_DEFAULT 32768
 // host-buffer calls of at most this many signatures skip the H2D / D2H copies:
 // the latency kernel reads the gathered inputs from, and writes the verdicts
 // to, fine-grained page-locked host memory (one launch per call instead of
@@ -500,6 +507,7 @@ pv_tuning default_tuning() {
   t.host_copy_threads = PV_HOST_COPY_THREADS;
   t.host_ramp = PV_HOST_RAMP;
   t.host_pin_max_mb = (uint32_t)(PV_HOST_PIN_MAX >> 20);
+  t.bls_quad_max = PV_BLS_QUAD_MAX_DEFAULT;
   return t;
 }
 pv_tuning g_tune = default_tuning();
@@ -521,6 +529,7 @@ int check_tuning(const pv_tuning& t) {
   if (t.host_pin_max_mb < 16 || t.host_pin_max_mb > 4096) return fail(PV_EINVAL, "host_pin_max_mb must be in 16..4096");
   if (t.host_trace > 1) return fail(PV_EINVAL, "host_trace must be 0 or 1");
   if (t.test_dup_devices == 1 || t.test_dup_devices > 8) return fail(PV_EINVAL, "test_dup_devices must be 0 or 2..8");
+  if (t.bls_quad_max > (1u << 20)) return fail(PV_EINVAL, "bls_quad_max must be <= 2^20");
   return PV_OK;
 }
 
@@ -1653,6 +1662,7 @@ int pv_set_tuning(const pv_tuning* t) {
   if (dup_changed && !g_devs.empty())
     return fail(PV_EINVAL, "test_dup_devices is read by pv_init: call pv_shutdown first");
   g_tune = *t;
+  pvbls::set_quad_max(g_tune.bls_quad_max);
   DeviceGuard dg;
   for (auto& d : g_devs) apply_tuning(d, g_tune);
   return PV_OK;

@@ -20,6 +20,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -48,13 +49,17 @@ constexpr uint32_t BLS_WAVE_CHECKS = 64;   // checks per wave (= the key segment
 #else
 constexpr uint32_t BLS_WAVE_CHECKS = 32;
 #endif
-// calls of at most this many checks run one check per lane QUAD
-// (k_bls_verify_quad: the two Miller loops on two lane pairs, 16 checks per
-// wave): a lone check's chain is a third shorter, the total work larger
+// calls of at most pv_tuning.bls_quad_max checks (default PV_BLS_QUAD_MAX) run
+// one check per lane QUAD (k_bls_verify_quad: the two Miller loops on two lane
+// pairs, the final exponentiation's products split over both, 16 checks per
+// wave): a lone check's chain is ~30 % shorter, the total work larger (the
+// Miller loop's squarings run on both pairs); from ~50k checks the pair kernel
+// is faster (profiles/r04g_bls_latency_quad_threshold.jsonl)
 #ifndef PV_BLS_QUAD_MAX
-#define PV_BLS_QUAD_MAX 8192
+#define PV_BLS_QUAD_MAX 32768
 #endif
-constexpr uint64_t BLS_QUAD_MAX = PV_BLS_QUAD_MAX;
+std::atomic<uint64_t> g_quad_max{PV_BLS_QUAD_MAX};
+void set_quad_max(uint64_t n) { g_quad_max.store(n); }
 constexpr uint32_t BLS_QUAD_CHECKS = 16;
 
 __device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
@@ -540,7 +545,7 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
 #ifdef PV_BLS_ONE_LANE
   const uint32_t pad = BLS_WAVE_CHECKS;
 #else
-  const bool quad = n <= BLS_QUAD_MAX;
+  const bool quad = n <= g_quad_max.load();
   const uint32_t pad = quad ? BLS_QUAD_CHECKS : BLS_WAVE_CHECKS;
 #endif
   const uint64_t slots = ((n + pad - 1) / pad + ks.nkeys) * pad;

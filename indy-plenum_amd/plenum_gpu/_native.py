@@ -116,7 +116,7 @@ class Tuning(ctypes.Structure):
                 ('host_fused', ctypes.c_uint32), ('host_staging', ctypes.c_uint32), ('host_chunks', ctypes.c_uint32),
                 ('host_first_pct', ctypes.c_uint32), ('host_copy_threads', ctypes.c_uint32),
                 ('host_ramp', ctypes.c_uint64), ('host_pin_max_mb', ctypes.c_uint32), ('host_trace', ctypes.c_uint32),
-                ('test_dup_devices', ctypes.c_uint32), ('reserved', ctypes.c_uint32)]
+                ('test_dup_devices', ctypes.c_uint32), ('bls_quad_max', ctypes.c_uint32)]
 
 
 CURVE_MODES = {0: 'half', 1: 'full', 2: 'grouped'}   # PV_CURVE_HALF / _FULL / _GROUPED
@@ -130,7 +130,7 @@ def get_tuning():
     """The current pv_tuning as a dict (names of include/plenum_verify.h)."""
     t = Tuning(struct_size=ctypes.sizeof(Tuning))
     _check('pv_get_tuning', load().pv_get_tuning(ctypes.byref(t)))
-    return {f: getattr(t, f) for f, _ in Tuning._fields_ if f not in ('struct_size', 'reserved')}
+    return {f: getattr(t, f) for f, _ in Tuning._fields_ if f != 'struct_size'}
 
 
 def set_tuning(**kw):

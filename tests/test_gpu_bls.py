@@ -174,10 +174,14 @@ def test_10k_checks_vs_oracle(fx, nat, orc):
     assert 0.85 * n < got.sum() < 0.95 * n
     h_ms, v_ms = nat.bls_kernel_ms()
     assert v_ms > 0
-    # 10k checks take the lane-pair kernel; a call of at most 8,192 the lane-quad
-    # kernel (pv_bls.hip BLS_QUAD_MAX): the same verdicts on a 3,001-check subset
-    sub = nat.bls_verify_arrays(sig[:3001], blob, off, midx[:3001], kidx[:3001])
-    assert (sub == got[:3001]).all(), np.nonzero(sub != got[:3001])[0][:10]
+    # 10k checks take the lane-quad kernel by default (pv_tuning.bls_quad_max =
+    # 32768); with bls_quad_max = 0 the lane-pair kernel: the same verdicts
+    prev = nat.set_tuning(bls_quad_max=0)
+    try:
+        pair = nat.bls_verify_arrays(sig, blob, off, midx, kidx)
+    finally:
+        nat.set_tuning(**prev)
+    assert (pair == got).all(), np.nonzero(pair != got)[0][:10]
 
 
 def test_commit_batch_and_quorum(fx, nat):
