@@ -334,6 +334,10 @@ int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *
  *   bls_quad_max    BLS calls (pv_bls_verify_*) of at most this many checks run
  *                   one check per lane quad (latency), larger ones one per lane
  *                   pair (throughput).  Default 32768 (0..2^20).
+ *   bls_oct_max     BLS calls of at most this many checks run one check per lane
+ *                   octet (the shortest chain; takes precedence over
+ *                   bls_quad_max).  Default 4096 (0..2^20).
+ *   reserved        must be 0.
  *   test_dup_devices  TEST ONLY, read by the next pv_init: 2..8 opens that many
  *                   engine devices, all on HIP device 0, so the multi-device
  *                   paths (a worker thread per device, shard offsets, error
@@ -368,6 +372,8 @@ typedef struct pv_tuning {
   uint32_t host_trace;
   uint32_t test_dup_devices;
   uint32_t bls_quad_max;
+  uint32_t bls_oct_max;
+  uint32_t reserved;
 } pv_tuning;
 int pv_get_tuning(pv_tuning *t);
 int pv_set_tuning(const pv_tuning *t);

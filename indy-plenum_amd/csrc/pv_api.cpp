@@ -31,6 +31,7 @@ static_assert(PV_KEY_WORDS_WIDE == (unsigned)pv::KEYTAB_WIDE_WORDS, "wide prepar
 
 namespace pvbls {
 void set_quad_max(uint64_t n);   // pv_bls.hip
+void set_oct_max(uint64_t n);
 }
 
 namespace {
@@ -65,6 +66,8 @@ int fail(int code, const char* fmt, ...) {
 // BLS calls of at most this many checks run the lane-quad check kernel
 // (pv_bls.hip; the same default as its PV_BLS_QUAD_MAX); tuning.bls_quad_max
 #define PV_BLS_QUAD_MAX_DEFAULT 32768
+// ... and calls of at most this many the lane-octet kernel; tuning.bls_oct_max
+#define PV_BLS_OCT_MAX_DEFAULT 4096
 // host-buffer calls of at most this many signatures skip the H2D / D2H copies:
 // the latency kernel reads the gathered inputs from, and writes the verdicts
 // to, fine-grained page-locked host memory (one launch per call instead of
@@ -508,6 +511,7 @@ pv_tuning default_tuning() {
   t.host_ramp = PV_HOST_RAMP;
   t.host_pin_max_mb = (uint32_t)(PV_HOST_PIN_MAX >> 20);
   t.bls_quad_max = PV_BLS_QUAD_MAX_DEFAULT;
+  t.bls_oct_max = PV_BLS_OCT_MAX_DEFAULT;
   return t;
 }
 pv_tuning g_tune = default_tuning();
@@ -529,7 +533,9 @@ int check_tuning(const pv_tuning& t) {
   if (t.host_pin_max_mb < 16 || t.host_pin_max_mb > 4096) return fail(PV_EINVAL, "host_pin_max_mb must be in 16..4096");
   if (t.host_trace > 1) return fail(PV_EINVAL, "host_trace must be 0 or 1");
   if (t.test_dup_devices == 1 || t.test_dup_devices > 8) return fail(PV_EINVAL, "test_dup_devices must be 0 or 2..8");
-  if (t.bls_quad_max > (1u << 20)) return fail(PV_EINVAL, "bls_quad_max must be <= 2^20");
+  if (t.bls_quad_max > (1u << 20) || t.bls_oct_max > (1u << 20))
+    return fail(PV_EINVAL, "bls_quad_max / bls_oct_max must be <= 2^20");
+  if (t.reserved != 0) return fail(PV_EINVAL, "reserved must be 0");
   return PV_OK;
 }
 
@@ -1663,6 +1669,7 @@ int pv_set_tuning(const pv_tuning* t) {
     return fail(PV_EINVAL, "test_dup_devices is read by pv_init: call pv_shutdown first");
   g_tune = *t;
   pvbls::set_quad_max(g_tune.bls_quad_max);
+  pvbls::set_oct_max(g_tune.bls_oct_max);
   DeviceGuard dg;
   for (auto& d : g_devs) apply_tuning(d, g_tune);
   return PV_OK;

@@ -61,6 +61,16 @@ constexpr uint32_t BLS_WAVE_CHECKS = 32;
 std::atomic<uint64_t> g_quad_max{PV_BLS_QUAD_MAX};
 void set_quad_max(uint64_t n) { g_quad_max.store(n); }
 constexpr uint32_t BLS_QUAD_CHECKS = 16;
+// calls of at most pv_tuning.bls_oct_max checks (default PV_BLS_OCT_MAX) run one
+// check per lane OCTET (k_bls_verify_oct: the quad schedule with every step's
+// products split between two quads, 8 checks per wave): the shortest chain, the
+// most work per check
+#ifndef PV_BLS_OCT_MAX
+#define PV_BLS_OCT_MAX 4096
+#endif
+std::atomic<uint64_t> g_oct_max{PV_BLS_OCT_MAX};
+void set_oct_max(uint64_t n) { g_oct_max.store(n); }
+constexpr uint32_t BLS_OCT_CHECKS = 8;
 
 __device__ __forceinline__ void st_fp(uint32_t* w, const fp& a) {
 #pragma unroll
@@ -343,6 +353,41 @@ __global__ __launch_bounds__(BLS_BLOCK, 2) void k_bls_verify_quad(
   const bool ok = bls_check_quad_q(mp_slot(), q, s_inf, st == 1, g_lines, pk_lines);
   if (live && (threadIdx.x & 3) == 0) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
 }
+
+// one check per lane OCTET (lanes 8c .. 8c + 7; the smallest calls): the quad
+// kernel's roles (pair 0 e(sigma, g), pair 1 e(-H, pk)) in each of two quads,
+// which split every step's Fp2 products between them (bls_check_oct_q).  8
+// checks per wave, slots of `order` padded to 8 per key.
+__global__ __launch_bounds__(BLS_BLOCK, 2) void k_bls_verify_oct(
+    const uint8_t* __restrict__ sig, const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ key_idx,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ total, const uint32_t* __restrict__ msgtab,
+    const uint32_t* __restrict__ lines, const uint8_t* __restrict__ kstatus, uint32_t n_msgs,
+    const uint32_t* __restrict__ prep, uint64_t n, uint8_t* __restrict__ verdict) {
+  const uint32_t slot = (blockIdx.x * BLS_BLOCK + threadIdx.x) >> 3;
+  const int h = threadIdx.x & 1, own = (threadIdx.x >> 1) & 1;
+  const uint32_t task0 = __builtin_amdgcn_readfirstlane(slot & ~(BLS_OCT_CHECKS - 1));
+  if (task0 >= *total) return;
+  const uint32_t j = order[slot];
+  const bool live = j != 0xffffffffu;
+  const uint32_t key = __builtin_amdgcn_readfirstlane(live ? key_idx[j] : 0u);
+  const uint32_t* g_lines = lines;
+  const uint32_t* pk_lines = lines + (uint64_t)KEY_LINE_WORDS * (1 + key);
+  const uint8_t st = kstatus[1 + key];
+  p1 q[2] = {{fzero()}, {fzero()}};   // q[0]: this pair's point (sigma for pair 0, -H for pair 1)
+  bool s_inf = true;
+  const bool msg_ok = live && msg_idx[j] < n_msgs;
+  if (live) {
+    s_inf = prep[2 * NL * n + j] != 0;
+    if (own == 0) {
+#pragma unroll
+      for (int w = 0; w < NL; ++w) q[0].e[0].l[w] = (int32_t)prep[(h * NL + w) * n + j];
+    } else if (st == 0 && msg_ok) {
+      q[0].e[0] = ld_fp(msgtab + (uint64_t)MSG_WORDS * msg_idx[j] + (2 + h) * NL);
+    }
+  }
+  const bool ok = bls_check_oct_q(q, s_inf, st == 1, g_lines, pk_lines);
+  if (live && (threadIdx.x & 7) == 0) verdict[j] = (st == 2 || !msg_ok) ? 0 : (uint8_t)ok;
+}
 #endif
 
 // Bls::verify_multi_sig's aggregated key (ursa: PointG2::new_inf() + every
@@ -545,8 +590,9 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
 #ifdef PV_BLS_ONE_LANE
   const uint32_t pad = BLS_WAVE_CHECKS;
 #else
-  const bool quad = n <= g_quad_max.load();
-  const uint32_t pad = quad ? BLS_QUAD_CHECKS : BLS_WAVE_CHECKS;
+  const bool oct = n <= g_oct_max.load();
+  const bool quad = !oct && n <= g_quad_max.load();
+  const uint32_t pad = oct ? BLS_OCT_CHECKS : quad ? BLS_QUAD_CHECKS : BLS_WAVE_CHECKS;
 #endif
   const uint64_t slots = ((n + pad - 1) / pad + ks.nkeys) * pad;
   BLS_HIP(d.msgtab.ensure(n_msgs * MSG_WORDS));
@@ -560,7 +606,7 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
 #endif
   BLS_HIP(hipEventRecord(d.ev[0], s));
 #ifndef PV_BLS_ONE_LANE
-  if (quad) {   // message hashing and sigma's prep in one launch (both timed as "hash")
+  if (quad || oct) {   // message hashing and sigma's prep in one launch (both timed as "hash")
     const uint32_t hb = blocks_for(8 * n_msgs, 64);
     if (n_msgs || n)
       hipLaunchKernelGGL(k_bls_prep, dim3(hb + blocks_for(n, 64)), dim3(64), 0, s, blob, off, (uint32_t)n_msgs, hb,
@@ -585,8 +631,12 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   hipLaunchKernelGGL(k_bls_verify, dim3(blocks_for(slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx, key_idx,
                      d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs, verdict);
 #else
-  if (n && !quad) hipLaunchKernelGGL(k_bls_sigprep, dim3(blocks_for(n, 64)), dim3(64), 0, s, sig, n, d.sigprep.p);
-  if (quad)
+  if (n && !quad && !oct) hipLaunchKernelGGL(k_bls_sigprep, dim3(blocks_for(n, 64)), dim3(64), 0, s, sig, n, d.sigprep.p);
+  if (oct)
+    hipLaunchKernelGGL(k_bls_verify_oct, dim3(blocks_for(8 * slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx,
+                       key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs,
+                       d.sigprep.p, n, verdict);
+  else if (quad)
     hipLaunchKernelGGL(k_bls_verify_quad, dim3(blocks_for(4 * slots, BLS_BLOCK)), dim3(BLS_BLOCK), 0, s, sig, msg_idx,
                        key_idx, d.order.p, d.total.p, d.msgtab.p, ks.lines.p, ks.kstatus.p, (uint32_t)n_msgs,
                        d.sigprep.p, n, verdict);

@@ -231,11 +231,96 @@ PV_HD fp6 f6mul_fold(const fp6& x, const fp6& y) {
   return fp6{f2norm(c0), f2norm(c1), f2norm(c2)};
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// ------------------------------------------------------------------ lane groups above the pair
+// k_bls_verify_quad runs a check over a lane QUAD (two pairs, qrole = lane bit 1),
+// k_bls_verify_oct over an OCTET (two quads, orole = lane bit 2); the other
+// pair's value of the same role crosses with quad_perm [2,3,0,1], the other
+// quad's with ds_swizzle (xor 4), both in group-uniform control flow
+__device__ __forceinline__ fp qx_fp(const fp& x) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = __builtin_amdgcn_mov_dpp(x.l[i], 0x4E, 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ fp2 qx_fp2(const fp2& x) { return fp2{qx_fp(x.a), qx_fp(x.b)}; }
+__device__ __forceinline__ p6 pqswap(const p6& x) {
+  const fp6& c = x.e[0];
+  p6 r;
+  r.e[0] = fp6{qx_fp2(c.c0), qx_fp2(c.c1), qx_fp2(c.c2)};
+  return r;
+}
+__device__ __forceinline__ bool qrole() { return (threadIdx.x >> 1) & 1; }
+__device__ __forceinline__ fp ox_fp(const fp& x) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = __builtin_amdgcn_ds_swizzle(x.l[i], 0x101F);   // and 0x1f, xor 4
+  return r;
+}
+__device__ __forceinline__ fp2 ox_fp2(const fp2& x) { return fp2{ox_fp(x.a), ox_fp(x.b)}; }
+__device__ __forceinline__ bool orole() { return (threadIdx.x >> 2) & 1; }
+template <int LV>
+__device__ __forceinline__ fp2 sx_fp2(const fp2& x) { return LV == 1 ? qx_fp2(x) : ox_fp2(x); }
+template <int LV>
+__device__ __forceinline__ bool srole() { return LV == 1 ? qrole() : orole(); }
+
+// f6mul_i's sums from the split products: the half g = 0 of the group level LV
+// holds the diagonal p = v0, v1, v2, the half g = 1 the Karatsuba sums s12, s01, s02
+template <int LV>
+__device__ __forceinline__ fp6 f6_sums(const fp2& p0, const fp2& p1, const fp2& p2) {
+  const bool g = srole<LV>();
+  const fp2 o0 = sx_fp2<LV>(p0), o1 = sx_fp2<LV>(p1), o2 = sx_fp2<LV>(p2);
+  const fp2 v0 = f2sel(g, o0, p0), v1 = f2sel(g, o1, p1), v2 = f2sel(g, o2, p2);
+  const fp2 s12 = f2sel(g, p0, o0), s01 = f2sel(g, p1, o1), s02 = f2sel(g, p2, o2);
+  fp6 r;
+  r.c0 = f2norm(f2addL(f2mulxiL(f2subL(f2subL(s12, v1), v2)), v0));
+  r.c1 = f2norm(f2addL(f2subL(f2subL(s01, v0), v1), f2mulxiL(v2)));
+  r.c2 = f2norm(f2addL(f2subL(f2subL(s02, v0), v2), v1));
+  return r;
+}
+// f6mul_i(x, y) with its six Fp2 products split over the level-LV halves
+template <int LV>
+__device__ __forceinline__ fp6 f6mul_s(const fp6& x, const fp6& y) {
+  const bool g = srole<LV>();
+  const fp2 p0 = pin(f2mul(f2sel(g, f2addL(x.c1, x.c2), x.c0), f2sel(g, f2add(y.c1, y.c2), y.c0)));
+  const fp2 p1 = pin(f2mul(f2sel(g, f2addL(x.c0, x.c1), x.c1), f2sel(g, f2add(y.c0, y.c1), y.c1)));
+  const fp2 p2 = pin(f2mul(f2sel(g, f2addL(x.c0, x.c2), x.c2), f2sel(g, f2add(y.c0, y.c2), y.c2)));
+  return f6_sums<LV>(p0, p1, p2);
+}
+__device__ __forceinline__ fp6 f6mul_q(const fp6& x, const fp6& y) { return f6mul_s<1>(x, y); }
+// the octet's Fp6 product split four ways: pair m's three products (as f6mul_q)
+// with the first on quad g = 0, the third on g = 1, the second on both
+__device__ __forceinline__ fp6 f6mul_o4(const fp6& x, const fp6& y) {
+  const bool m = qrole(), g = orole();
+  const fp2 xa0 = f2sel(m, f2addL(x.c1, x.c2), x.c0), ya0 = f2sel(m, f2add(y.c1, y.c2), y.c0);
+  const fp2 xa2 = f2sel(m, f2addL(x.c0, x.c2), x.c2), ya2 = f2sel(m, f2add(y.c0, y.c2), y.c2);
+  const fp2 pa = pin(f2mul(f2sel(g, xa2, xa0), f2sel(g, ya2, ya0)));
+  const fp2 p1 = pin(f2mul(f2sel(m, f2addL(x.c0, x.c1), x.c1), f2sel(m, f2add(y.c0, y.c1), y.c1)));
+  const fp2 oa = ox_fp2(pa);
+  return f6_sums<1>(f2sel(g, oa, pa), p1, f2sel(g, pa, oa));
+}
+// mp_f6mul01 split over the octet's quads: g = 0 forms m and t1, g = 1 t0 and t2,
+// both t3; the same sums (c0 = t0 + xi t3, c1 = m - t0 - t1, c2 = t1 + t2)
+template <int ST>
+__device__ __forceinline__ fp6 mo_f6mul01(pslot<ST> S, int half, const fp2& b0, const fp2& b1) {
+  const int X = 3 * half;
+  const bool g = orole();
+  const fp2 pa = pin(f2mul(f2sel(g, S.ld(X), f2addL(S.ld(X), S.ld(X + 1))), f2sel(g, b0, f2add(b0, b1))));
+  mp_fence();
+  const fp2 pb = pin(f2mul(S.ld(g ? X + 2 : X + 1), f2sel(g, b0, b1)));
+  mp_fence();
+  const fp2 t3 = pin(f2mul(S.ld(X + 2), b1));
+  const fp2 oa = ox_fp2(pa), ob = ox_fp2(pb);
+  const fp2 m = f2sel(g, oa, pa), t0 = f2sel(g, pa, oa), t1 = f2sel(g, ob, pb), t2 = f2sel(g, pb, ob);
+  return fp6{f2norm(f2addL(f2mulxiL(t3), t0)), f2norm(f2subL(f2subL(m, t1), t0)), f2norm(f2addL(t1, t2))};
+}
+#endif
+
 // f = f (1 + (b0 + b1 v) w), f12mul_line_i split: role 0 forms v (f.b l) and
 // writes f.a + v f.b l, role 1 forms f.a l and writes f.b + f.a l.  The line's
 // coefficients b0 = B' x_P (role 0) and b1 = C' y_P (role 1) are exchanged;
 // q holds each role's coordinate of P (x_P for role 0, y_P for role 1).
-template <int ST>
+template <int ST, bool OCT = false>
 PV_HD void mp_line(pslot<ST> S, const uint32_t* L, const p1& q) {
   p2 c;
 #pragma unroll
@@ -246,6 +331,9 @@ PV_HD void mp_line(pslot<ST> S, const uint32_t* L, const p1& q) {
   for (int j = 0; j < PL; ++j) {
     const int h = prole(j);
     const fp2 b0 = f2sel(h, o.e[j], c.e[j]), b1 = f2sel(h, c.e[j], o.e[j]);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (OCT) P.e[j] = mo_f6mul01(S, 1 - h, b0, b1); else
+#endif
     P.e[j] = mp_f6mul01(S, 1 - h, b0, b1);
   }
   mp_fence();
@@ -264,7 +352,7 @@ PV_HD void mp_line(pslot<ST> S, const uint32_t* L, const p1& q) {
 // f = f^2 (f12sqr_i's complex squaring split): role 0 forms s = (a + b)(a + v b),
 // role 1 t = a b; t crosses to role 0, which writes s - t - v t, role 1 writes
 // 2t (as p - (-p) - 0, the same integer as f2dbl)
-template <int ST>
+template <int ST, bool OCT = false>
 PV_HD fp6 mp_sqr_prod(pslot<ST> S, int h) {
   fp6 x, y;
   {
@@ -272,13 +360,16 @@ PV_HD fp6 mp_sqr_prod(pslot<ST> S, int h) {
     x = f6sel(h, a, f6add(a, b));
     y = f6sel(h, b, f6add(a, f6mulv(b)));
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (OCT) return f6mul_s<2>(x, y);   // the octet's quads split the six products
+#endif
   return f6mul_fold(x, y);
 }
-template <int ST>
+template <int ST, bool OCT = false>
 PV_HD void mp_sqr(pslot<ST> S) {
   p6 P;
 #pragma unroll
-  for (int j = 0; j < PL; ++j) P.e[j] = mp_sqr_prod(S, prole(j));
+  for (int j = 0; j < PL; ++j) P.e[j] = mp_sqr_prod<ST, OCT>(S, prole(j));
   mp_fence();
   const p6 Q = pswap(P);
 #pragma unroll
@@ -497,37 +588,6 @@ PV_HD bool pr_is_one(const p6& x) {
 // Every sum is the pair version's (the same integers, so the same limbs).  The
 // host build has no quad: there pmul / pcyc / preduce / pinv are the pair ops.
 #if defined(__HIP_DEVICE_COMPILE__)
-// the other lane pair's value of the same role (quad_perm [2,3,0,1])
-__device__ __forceinline__ fp qx_fp(const fp& x) {
-  fp r;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) r.l[i] = __builtin_amdgcn_mov_dpp(x.l[i], 0x4E, 0xf, 0xf, false);
-  return r;
-}
-__device__ __forceinline__ fp2 qx_fp2(const fp2& x) { return fp2{qx_fp(x.a), qx_fp(x.b)}; }
-__device__ __forceinline__ p6 pqswap(const p6& x) {
-  const fp6& c = x.e[0];
-  p6 r;
-  r.e[0] = fp6{qx_fp2(c.c0), qx_fp2(c.c1), qx_fp2(c.c2)};
-  return r;
-}
-__device__ __forceinline__ bool qrole() { return (threadIdx.x >> 1) & 1; }
-
-// f6mul_i(x, y) with its six Fp2 products split over the two pairs
-__device__ __forceinline__ fp6 f6mul_q(const fp6& x, const fp6& y) {
-  const bool g = qrole();
-  const fp2 p0 = pin(f2mul(f2sel(g, f2addL(x.c1, x.c2), x.c0), f2sel(g, f2add(y.c1, y.c2), y.c0)));
-  const fp2 p1 = pin(f2mul(f2sel(g, f2addL(x.c0, x.c1), x.c1), f2sel(g, f2add(y.c0, y.c1), y.c1)));
-  const fp2 p2 = pin(f2mul(f2sel(g, f2addL(x.c0, x.c2), x.c2), f2sel(g, f2add(y.c0, y.c2), y.c2)));
-  const fp2 o0 = qx_fp2(p0), o1 = qx_fp2(p1), o2 = qx_fp2(p2);
-  const fp2 v0 = f2sel(g, o0, p0), v1 = f2sel(g, o1, p1), v2 = f2sel(g, o2, p2);
-  const fp2 s12 = f2sel(g, p0, o0), s01 = f2sel(g, p1, o1), s02 = f2sel(g, p2, o2);
-  fp6 r;
-  r.c0 = f2norm(f2addL(f2mulxiL(f2subL(f2subL(s12, v1), v2)), v0));
-  r.c1 = f2norm(f2addL(f2subL(f2subL(s01, v0), v1), f2mulxiL(v2)));
-  r.c2 = f2norm(f2addL(f2subL(f2subL(s02, v0), v2), v1));
-  return r;
-}
 __device__ __noinline__ p6 pr_mul_q(const p6& x, const p6& y) {
   const int h = prole(0);
   const bool g = qrole();
@@ -610,79 +670,155 @@ __device__ __forceinline__ void mq_reduce(pslot<ST> S) {
   if (!g) S.st(e2, r2);
   mp_fence();
 }
+// ---- the octet (k_bls_verify_oct): the quad's split, each pair's share split
+// again between the two quads (orole g)
+// x y: of pair m's five products (its three of t, its m-product ma, and m2) quad
+// g = 0 forms t's first and second and m2, g = 1 t's third, ma and m2
+__device__ __noinline__ p6 pr_mul_o(const p6& x, const p6& y) {
+  const int h = prole(0);
+  const bool m = qrole(), g = orole();
+  const fp6 &xs = x.e[0], &ys = y.e[0];
+  p6 t;
+  p2 mm[3];
+  {
+    const p6 xo = pswap(x), yo = pswap(y);
+    const fp6 X = f6add(xs, xo.e[0]), Y = f6add(ys, yo.e[0]);
+    const fp2 t0x = f2sel(m, f2addL(xs.c1, xs.c2), xs.c0), t0y = f2sel(m, f2add(ys.c1, ys.c2), ys.c0);
+    const fp2 t1x = f2sel(m, f2addL(xs.c0, xs.c1), xs.c1), t1y = f2sel(m, f2add(ys.c0, ys.c1), ys.c1);
+    const fp2 t2x = f2sel(m, f2addL(xs.c0, xs.c2), xs.c2), t2y = f2sel(m, f2add(ys.c0, ys.c2), ys.c2);
+    const fp2 a0 = f2sel(h, f2addL(X.c1, X.c2), X.c0), b0 = f2sel(h, f2add(Y.c1, Y.c2), Y.c0);
+    const fp2 a1 = f2sel(h, f2addL(X.c0, X.c1), X.c1), b1 = f2sel(h, f2add(Y.c0, Y.c1), Y.c1);
+    const fp2 max = f2sel(m, a1, a0), may = f2sel(m, b1, b0);   // m0 (pair 0) / m1 (pair 1)
+    const fp2 pa = pin(f2mul(f2sel(g, t2x, t0x), f2sel(g, t2y, t0y)));   // t0 / t2
+    const fp2 pb = pin(f2mul(f2sel(g, max, t1x), f2sel(g, may, t1y)));   // t1 / ma
+    mm[2].e[0] = pin(f2mul(f2sel(h, f2addL(X.c0, X.c2), X.c2), f2sel(h, f2add(Y.c0, Y.c2), Y.c2)));
+    const fp2 oa = ox_fp2(pa), ob = ox_fp2(pb);
+    t.e[0] = f6_sums<1>(f2sel(g, oa, pa), f2sel(g, ob, pb), f2sel(g, pa, oa));
+    const fp2 ma = f2sel(g, pb, ob);
+    const fp2 mo = qx_fp2(ma);
+    mm[0].e[0] = f2sel(m, mo, ma);
+    mm[1].e[0] = f2sel(m, ma, mo);
+  }
+  return pr_mul_tail(t, mm);
+}
+__device__ __noinline__ p6 pr_inv_o(const p6& x) {
+  p6 sq;
+  sq.e[0] = f6mul_o4(x.e[0], x.e[0]);
+  const p6 so = pswap(sq);
+  const int h = prole(0);
+  const fp6 d = f6inv(f6sub(f6sel(h, so.e[0], sq.e[0]), f6mulv(f6sel(h, sq.e[0], so.e[0]))));
+  const fp6 m = f6mul_o4(x.e[0], d);
+  p6 r;
+  r.e[0] = f6sel(h, f6neg(m), m);
+  return r;
+}
+// mp_cyc_sqr over the octet's shared slot: quad g = 0 squares the Fp4 pair k = m,
+// g = 1 the pair k = 2 (written by pair 0 of that quad); every read before every write
+template <int ST>
+__device__ __forceinline__ void mo_cyc_sqr(pslot<ST> S) {
+  const int h = prole(0);
+  const bool m = qrole(), g = orole();
+  const fp2 z0 = S.ld(g ? 1 : (m ? 3 : 0)), z1 = S.ld(g ? 5 : (m ? 2 : 4));
+  const fp2 p = pin(f2mul(f2sel(h, z0, f2addL(z0, z1)), f2sel(h, z1, f2norm(f2addL(f2mulxiL(z1), z0)))));
+  const int e = g ? (h ? 3 : 2) : (h ? (m ? 5 : 4) : (m ? 1 : 0));
+  const fp2 zz = S.ld(e);
+  mp_fence();
+  const fp2 q = px_fp2(p);
+  const fp2 a = f2sel(g, f2sel(h, f2mulxiL(p), p), p);
+  const fp2 u = f2norm(f2subL(f2subL(a, f2sel(h, f2negL(a), q)), f2sel(h, f2zero(), f2mulxiL(q))));
+  const fp2 zs = f2sel(h, zz, f2negL(zz));
+  const fp2 out = f2norm(f2addL(f2addL(f2addL(u, u), u), f2addL(zs, zs)));
+  if (!(g && m)) S.st(e, out);
+  mp_fence();
+}
+template <int ST>
+__device__ __forceinline__ void mo_reduce(pslot<ST> S) {
+  const int h = prole(0);
+  const bool m = qrole(), g = orole();
+  const int e = 3 * h + (g ? 2 : (int)m);
+  const fp2 r = f2reduce(S.ld(e));
+  mp_fence();
+  if (!(g && m)) S.st(e, r);
+  mp_fence();
+}
 #endif
-template <bool Q>
+// the final exponentiation's operations at group level LV (0 pair, 1 quad, 2 octet)
+template <int LV>
 PV_HD p6 pmul(const p6& x, const p6& y) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (Q) return pr_mul_q(x, y);
+  if constexpr (LV == 1) return pr_mul_q(x, y);
+  if constexpr (LV == 2) return pr_mul_o(x, y);
 #endif
   return pr_mul(x, y);
 }
-template <bool Q>
+template <int LV>
 PV_HD p6 pinv(const p6& x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (Q) return pr_inv_q(x);
+  if constexpr (LV == 1) return pr_inv_q(x);
+  if constexpr (LV == 2) return pr_inv_o(x);
 #endif
   return pr_inv(x);
 }
-template <bool Q, int ST>
+template <int LV, int ST>
 PV_HD void pcyc(pslot<ST> S) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (Q) return mq_cyc_sqr(S);
+  if constexpr (LV == 1) return mq_cyc_sqr(S);
+  if constexpr (LV == 2) return mo_cyc_sqr(S);
 #endif
   mp_cyc_sqr(S);
 }
-template <bool Q, int ST>
+template <int LV, int ST>
 PV_HD void preduce(pslot<ST> S) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (Q) return mq_reduce(S);
+  if constexpr (LV == 1) return mq_reduce(S);
+  if constexpr (LV == 2) return mo_reduce(S);
 #endif
   mp_reduce(S);
 }
 
 // x^u in the cyclotomic subgroup (cyc_pow_u's chain) with the power in the slot
-template <int ST, bool Q = false>
+template <int ST, int LV = 0>
 PV_BN_CALL p6 pr_pow_u(pslot<ST> S, const p6& x) {
   mp_put(S, x);
   for (int i = 0; i < 7; ++i) {
-    pcyc<Q>(S);
-    if ((i & 3) == 3) preduce<Q>(S);
+    pcyc<LV>(S);
+    if ((i & 3) == 3) preduce<LV>(S);
   }
-  mp_put(S, pmul<Q>(mp_get(S), x));   // x^(2^7 + 1)
+  mp_put(S, pmul<LV>(mp_get(S), x));   // x^(2^7 + 1)
   for (int i = 0; i < 55; ++i) {
-    pcyc<Q>(S);
-    if ((i & 3) == 3) preduce<Q>(S);
+    pcyc<LV>(S);
+    if ((i & 3) == 3) preduce<LV>(S);
   }
-  return pr_conj(pmul<Q>(mp_get(S), x));   // x^(2^62 + 2^55 + 1), conjugated
+  return pr_conj(pmul<LV>(mp_get(S), x));   // x^(2^62 + 2^55 + 1), conjugated
 }
-template <int ST, bool Q = false>
+template <int ST, int LV = 0>
 PV_BN_CALL p6 pr_cyc_sqr(pslot<ST> S, const p6& x) {
   mp_put(S, x);
-  pcyc<Q>(S);
+  pcyc<LV>(S);
   return mp_get(S);
 }
 
 // final_exp's chain on halves
-template <int ST, bool Q = false>
+template <int ST, int LV = 0>
 PV_BN_CALL p6 pr_final_exp(pslot<ST> S, const p6& f0) {
-  p6 f = pmul<Q>(pr_conj(f0), pinv<Q>(f0));   // ^(p^6 - 1)
-  f = pmul<Q>(pr_frob2(f), f);              // ^(p^2 + 1)
-  const p6 fu = pr_pow_u<ST, Q>(S, f);
-  const p6 fu2 = pr_pow_u<ST, Q>(S, fu);
-  const p6 fu3 = pr_pow_u<ST, Q>(S, fu2);
-  const p6 y6 = pr_conj(pmul<Q>(fu3, pr_frob1(fu3)));
-  p6 t0 = pr_cyc_sqr<ST, Q>(S, y6);
-  t0 = pmul<Q>(t0, pr_conj(pmul<Q>(fu, pr_frob1(fu2))));   // y4
+  p6 f = pmul<LV>(pr_conj(f0), pinv<LV>(f0));   // ^(p^6 - 1)
+  f = pmul<LV>(pr_frob2(f), f);              // ^(p^2 + 1)
+  const p6 fu = pr_pow_u<ST, LV>(S, f);
+  const p6 fu2 = pr_pow_u<ST, LV>(S, fu);
+  const p6 fu3 = pr_pow_u<ST, LV>(S, fu2);
+  const p6 y6 = pr_conj(pmul<LV>(fu3, pr_frob1(fu3)));
+  p6 t0 = pr_cyc_sqr<ST, LV>(S, y6);
+  t0 = pmul<LV>(t0, pr_conj(pmul<LV>(fu, pr_frob1(fu2))));   // y4
   const p6 y5 = pr_conj(fu2);
-  t0 = pmul<Q>(t0, y5);
-  p6 t1 = pmul<Q>(pmul<Q>(pr_conj(pr_frob1(fu)), y5), t0);
-  t0 = pmul<Q>(t0, pr_frob2(fu2));
-  t1 = pmul<Q>(pr_cyc_sqr<ST, Q>(S, t1), t0);
-  t1 = pr_cyc_sqr<ST, Q>(S, t1);
-  t0 = pmul<Q>(t1, pr_conj(f));
-  const p6 y0 = pmul<Q>(pmul<Q>(pr_frob1(f), pr_frob2(f)), pr_frob3(f));
-  t1 = pmul<Q>(t1, y0);
-  return pmul<Q>(pr_cyc_sqr<ST, Q>(S, t0), t1);
+  t0 = pmul<LV>(t0, y5);
+  p6 t1 = pmul<LV>(pmul<LV>(pr_conj(pr_frob1(fu)), y5), t0);
+  t0 = pmul<LV>(t0, pr_frob2(fu2));
+  t1 = pmul<LV>(pr_cyc_sqr<ST, LV>(S, t1), t0);
+  t1 = pr_cyc_sqr<ST, LV>(S, t1);
+  t0 = pmul<LV>(t1, pr_conj(f));
+  const p6 y0 = pmul<LV>(pmul<LV>(pr_frob1(f), pr_frob2(f)), pr_frob3(f));
+  t1 = pmul<LV>(t1, y0);
+  return pmul<LV>(pr_cyc_sqr<ST, LV>(S, t0), t1);
 }
 
 #if defined(__HIPCC__)
@@ -705,7 +841,10 @@ __device__ __forceinline__ pslot<MP_CHECKS> mp_slot() {
 // ONE pairing's Miller loop -- pair 0 over the generator's lines with sigma's
 // point, pair 1 over the key's lines with -H's -- with its point in q[0]; on the
 // host the caller passes that pairing's lines as g_lines.
-template <int ST, bool QUAD = false>
+// OCT (k_bls_verify_oct, one check over eight lanes): QUAD's schedule with each
+// step's Fp2 products split between the octet's two quads (mp_sqr / mp_line's
+// OCT forms), both quads on the same slot.
+template <int ST, bool QUAD = false, bool OCT = false>
 PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_lines, const p1 (&q)[2]) {
 #pragma unroll
   for (int j = 0; j < PL; ++j) S.st6(prole(j), prole(j) ? f6zero() : f6one());
@@ -744,8 +883,8 @@ PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_li
     for (int add = 0; add < 2; ++add) {
       if (add && !ate_bit(i)) break;
       fetch(k + 1);
-      if (!add && i != 63) mp_sqr(S);
-      mp_line(S, Lg(k), q[0]);
+      if (!add && i != 63) mp_sqr<ST, OCT>(S);
+      mp_line<ST, OCT>(S, Lg(k), q[0]);
       if (!QUAD) mp_line(S, Lp(k), q[1]);
       stash(k + 1);
       ++k;
@@ -754,7 +893,7 @@ PV_HD p6 miller_pair(pslot<ST> S, const uint32_t* g_lines, const uint32_t* pk_li
   mp_put(S, pr_conj(mp_get(S)));
   for (int j = 0; j < 2; ++j, ++k) {
     fetch(k + 1);
-    mp_line(S, Lg(k), q[0]);
+    mp_line<ST, OCT>(S, Lg(k), q[0]);
     if (!QUAD) mp_line(S, Lp(k), q[1]);
     stash(k + 1);
   }
@@ -784,7 +923,28 @@ __device__ __forceinline__ bool bls_check_quad_q(pslot<MP_CHECKS> S, const p1 (&
   const bool g = qrole();
   const p6 fs = g ? o : f, fh = g ? f : o;
   const pslot<MP_CHECKS> Sq{S.c & ~1u};   // the even pair's slot, shared by the quad
-  const bool one = pr_is_one(pr_final_exp<MP_CHECKS, true>(Sq, pr_mul_q(fs, fh)));
+  const bool one = pr_is_one(pr_final_exp<MP_CHECKS, 1>(Sq, pr_mul_q(fs, fh)));
+  if (s_inf || pk_inf) return s_inf && pk_inf;
+  return one;
+#else
+  return false;
+#endif
+}
+#endif
+#if defined(__HIPCC__)
+// the check over a lane OCTET (k_bls_verify_oct, the smallest calls): the quad
+// schedule with every step's products split between the octet's quads; the
+// Miller slots are per (check, pairing), shared by the two quads
+__device__ __forceinline__ bool bls_check_oct_q(const p1 (&q)[2], bool s_inf, bool pk_inf, const uint32_t* g_lines,
+                                                const uint32_t* pk_lines) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t col = ((threadIdx.x >> 3) << 1) | ((threadIdx.x >> 1) & 1u);
+  const p6 f = miller_pair<MP_CHECKS, true, true>(pslot<MP_CHECKS>{col}, g_lines, pk_lines, q);
+  const p6 o = pqswap(f);
+  const bool m = qrole();
+  const p6 fs = m ? o : f, fh = m ? f : o;
+  const pslot<MP_CHECKS> Sq{col & ~1u};   // the octet's shared slot
+  const bool one = pr_is_one(pr_final_exp<MP_CHECKS, 2>(Sq, pr_mul_o(fs, fh)));
   if (s_inf || pk_inf) return s_inf && pk_inf;
   return one;
 #else

@@ -116,7 +116,8 @@ class Tuning(ctypes.Structure):
                 ('host_fused', ctypes.c_uint32), ('host_staging', ctypes.c_uint32), ('host_chunks', ctypes.c_uint32),
                 ('host_first_pct', ctypes.c_uint32), ('host_copy_threads', ctypes.c_uint32),
                 ('host_ramp', ctypes.c_uint64), ('host_pin_max_mb', ctypes.c_uint32), ('host_trace', ctypes.c_uint32),
-                ('test_dup_devices', ctypes.c_uint32), ('bls_quad_max', ctypes.c_uint32)]
+                ('test_dup_devices', ctypes.c_uint32), ('bls_quad_max', ctypes.c_uint32),
+                ('bls_oct_max', ctypes.c_uint32), ('reserved', ctypes.c_uint32)]
 
 
 CURVE_MODES = {0: 'half', 1: 'full', 2: 'grouped'}   # PV_CURVE_HALF / _FULL / _GROUPED
@@ -130,7 +131,7 @@ def get_tuning():
     """The current pv_tuning as a dict (names of include/plenum_verify.h)."""
     t = Tuning(struct_size=ctypes.sizeof(Tuning))
     _check('pv_get_tuning', load().pv_get_tuning(ctypes.byref(t)))
-    return {f: getattr(t, f) for f, _ in Tuning._fields_ if f != 'struct_size'}
+    return {f: getattr(t, f) for f, _ in Tuning._fields_ if f not in ('struct_size', 'reserved')}
 
 
 def set_tuning(**kw):
@@ -154,7 +155,8 @@ ENV_TUNING = {'PV_CURVE_MODE': ('curve_mode', {v: k for k, v in CURVE_MODES.item
               'PV_HOST_STAGING': ('host_staging', {v: k for k, v in STAGING_MODES.items()}.get),
               'PV_HOST_CHUNKS': ('host_chunks', int), 'PV_HOST_FIRST_PCT': ('host_first_pct', int),
               'PV_HOST_COPY_THREADS': ('host_copy_threads', int), 'PV_HOST_RAMP': ('host_ramp', int),
-              'PV_HOST_PIN_MAX_MB': ('host_pin_max_mb', int), 'PV_HOST_TRACE': ('host_trace', int)}
+              'PV_HOST_PIN_MAX_MB': ('host_pin_max_mb', int), 'PV_HOST_TRACE': ('host_trace', int),
+              'PV_BLS_QUAD_MAX': ('bls_quad_max', int), 'PV_BLS_OCT_MAX': ('bls_oct_max', int)}
 
 
 def tuning_from_env(environ=None):

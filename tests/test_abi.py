@@ -108,13 +108,13 @@ def test_library_reads_no_environment(native):
     assert d == {'curve_mode': 0, 'lat_max': 32768, 'lat_keyed_max': 8192, 'small_zc_max': 2048, 'lat_kernel': 0,
                  'host_fused': 1, 'host_staging': 0, 'host_chunks': 8, 'host_first_pct': 50, 'host_copy_threads': 8,
                  'host_ramp': 32768, 'host_pin_max_mb': 512, 'host_trace': 0, 'test_dup_devices': 0,
-                 'bls_quad_max': 32768}
+                 'bls_quad_max': 32768, 'bls_oct_max': 4096}
     os.environ['PV_CURVE_MODE'] = 'full'        # ignored by the library itself
     try:
         assert native.get_tuning()['curve_mode'] == 0
         for bad in ({'curve_mode': 3}, {'host_chunks': 0}, {'host_ramp': 5}, {'test_dup_devices': 1},
                     {'host_pin_max_mb': 8}, {'lat_max': (1 << 20) + 1},
-                    {'bls_quad_max': (1 << 20) + 1}):
+                    {'bls_quad_max': (1 << 20) + 1}, {'bls_oct_max': (1 << 20) + 1}):
             with pytest.raises(native.PlenumGpuError):
                 native.set_tuning(**bad)
             assert native.get_tuning() == d

@@ -175,13 +175,15 @@ def test_10k_checks_vs_oracle(fx, nat, orc):
     h_ms, v_ms = nat.bls_kernel_ms()
     assert v_ms > 0
     # 10k checks take the lane-quad kernel by default (pv_tuning.bls_quad_max =
-    # 32768); with bls_quad_max = 0 the lane-pair kernel: the same verdicts
-    prev = nat.set_tuning(bls_quad_max=0)
-    try:
-        pair = nat.bls_verify_arrays(sig, blob, off, midx, kidx)
-    finally:
-        nat.set_tuning(**prev)
-    assert (pair == got).all(), np.nonzero(pair != got)[0][:10]
+    # 32768, bls_oct_max = 4096); the lane-pair kernel (both 0) and the lane-octet
+    # kernel (bls_oct_max above n) give the same verdicts
+    for kw in ({'bls_quad_max': 0, 'bls_oct_max': 0}, {'bls_oct_max': 1 << 20}):
+        prev = nat.set_tuning(**kw)
+        try:
+            other = nat.bls_verify_arrays(sig, blob, off, midx, kidx)
+        finally:
+            nat.set_tuning(**prev)
+        assert (other == got).all(), (kw, np.nonzero(other != got)[0][:10])
 
 
 def test_commit_batch_and_quorum(fx, nat):

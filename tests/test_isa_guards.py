@@ -90,7 +90,7 @@ def test_bls_check_kernel_reads_lines_with_vector_loads(disasm):
         name = disasm[i].split('<')[1].rstrip('>:')
         bodies[name] = disasm[i:fn[k + 1] if k + 1 < len(fn) else len(disasm)]
     verify = [n for n in bodies if 'k_bls_verify' in n]
-    assert len(verify) == 2    # the lane-pair and lane-quad check kernels
+    assert len(verify) == 3    # the lane-pair, lane-quad and lane-octet check kernels
     for v in verify:
         smem = [ln for ln in bodies[v] if re.search(r'\ss_load_', ln)]
         assert smem and len(smem) <= 16, smem
