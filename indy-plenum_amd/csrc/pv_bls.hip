@@ -121,9 +121,36 @@ __global__ __launch_bounds__(64) void k_bls_hash(const uint8_t* __restrict__ blo
 
 // grouping by key: count, padded segment starts (aligned to the checks per wave), scatter
 // a check whose key index is out of range is never scheduled: its verdict stays 0
-__global__ void k_bls_count(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys, uint32_t* __restrict__ cnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && key_idx[i] < nkeys) atomicAdd(cnt + key_idx[i], 1u);
+// Key sets of at most GROUP_LOCAL_KEYS keys (node keys: 4..100s) are counted per
+// block in LDS first, GROUP_PER_THREAD checks per thread, so that a 25-key set
+// takes one global atomic per key per 2,048 checks instead of one per check (2.5M
+// atomics on 25 addresses serialised in L2: 2.7 ms each for count and scatter).
+constexpr uint32_t GROUP_LOCAL_KEYS = 2048;
+constexpr int GROUP_PER_THREAD = 8;
+constexpr uint32_t GROUP_BLOCK = 256;
+__global__ __launch_bounds__(GROUP_BLOCK) void k_bls_count(const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                           uint32_t nkeys, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t lc[GROUP_LOCAL_KEYS];
+  const uint64_t base = (uint64_t)blockIdx.x * GROUP_BLOCK * GROUP_PER_THREAD + threadIdx.x;
+  if (nkeys > GROUP_LOCAL_KEYS) {   // block-uniform: global atomics per check
+    for (int e = 0; e < GROUP_PER_THREAD; ++e) {
+      const uint64_t i = base + (uint64_t)e * GROUP_BLOCK;
+      if (i < n && key_idx[i] < nkeys) atomicAdd(cnt + key_idx[i], 1u);
+    }
+    return;
+  }
+  for (uint32_t k = threadIdx.x; k < nkeys; k += GROUP_BLOCK) lc[k] = 0;
+  __syncthreads();
+  for (int e = 0; e < GROUP_PER_THREAD; ++e) {
+    const uint64_t i = base + (uint64_t)e * GROUP_BLOCK;
+    if (i < n) {
+      const uint32_t key = key_idx[i];
+      if (key < nkeys) atomicAdd(&lc[key], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nkeys; k += GROUP_BLOCK)
+    if (lc[k]) atomicAdd(cnt + k, lc[k]);
 }
 
 __global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uint32_t pad, uint32_t* __restrict__ seg,
@@ -137,14 +164,39 @@ __global__ void k_bls_segments(const uint32_t* __restrict__ cnt, uint32_t k, uin
   *total = s;
 }
 
-__global__ void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
-                              const uint32_t* __restrict__ seg, uint32_t* __restrict__ cursor,
-                              uint32_t* __restrict__ order) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t key = key_idx[i];
-  if (key >= nkeys) return;
-  order[seg[key] + atomicAdd(cursor + key, 1u)] = (uint32_t)i;
+// scatter: each check's rank within its block and key from an LDS atomic, one
+// global atomic per key per block reserves the block's range of the key's segment
+__global__ __launch_bounds__(GROUP_BLOCK) void k_bls_scatter(const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                             uint32_t nkeys, const uint32_t* __restrict__ seg,
+                                                             uint32_t* __restrict__ cursor,
+                                                             uint32_t* __restrict__ order) {
+  __shared__ uint32_t lc[GROUP_LOCAL_KEYS];
+  const uint64_t base = (uint64_t)blockIdx.x * GROUP_BLOCK * GROUP_PER_THREAD + threadIdx.x;
+  if (nkeys > GROUP_LOCAL_KEYS) {   // block-uniform: global atomics per check
+    for (int e = 0; e < GROUP_PER_THREAD; ++e) {
+      const uint64_t i = base + (uint64_t)e * GROUP_BLOCK;
+      if (i >= n) continue;
+      const uint32_t key = key_idx[i];
+      if (key < nkeys) order[seg[key] + atomicAdd(cursor + key, 1u)] = (uint32_t)i;
+    }
+    return;
+  }
+  for (uint32_t k = threadIdx.x; k < nkeys; k += GROUP_BLOCK) lc[k] = 0;
+  __syncthreads();
+  uint32_t key[GROUP_PER_THREAD], rank[GROUP_PER_THREAD];
+#pragma unroll
+  for (int e = 0; e < GROUP_PER_THREAD; ++e) {
+    const uint64_t i = base + (uint64_t)e * GROUP_BLOCK;
+    key[e] = i < n ? key_idx[i] : nkeys;
+    rank[e] = key[e] < nkeys ? atomicAdd(&lc[key[e]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nkeys; k += GROUP_BLOCK)
+    if (lc[k]) lc[k] = seg[k] + atomicAdd(cursor + k, lc[k]);   // the block's first slot of key k
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < GROUP_PER_THREAD; ++e)
+    if (key[e] < nkeys) order[lc[key[e]] + rank[e]] = (uint32_t)(base + (uint64_t)e * GROUP_BLOCK);
 }
 
 #ifdef PV_BLS_ONE_LANE
@@ -621,9 +673,12 @@ int enqueue_verify(BlsDev& d, const KeySet& ks, const uint8_t* sig, const uint8_
   BLS_HIP(hipMemsetAsync(d.cnt.p, 0, ks.nkeys * 4, s));
   BLS_HIP(hipMemsetAsync(d.cursor.p, 0, ks.nkeys * 4, s));
   BLS_HIP(hipMemsetAsync(d.order.p, 0xff, slots * 4, s));
-  hipLaunchKernelGGL(k_bls_count, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, ks.nkeys, d.cnt.p);
+  const unsigned gblocks = blocks_for(n, GROUP_BLOCK * GROUP_PER_THREAD);
+  if (gblocks)
+    hipLaunchKernelGGL(k_bls_count, dim3(gblocks), dim3(GROUP_BLOCK), 0, s, key_idx, n, ks.nkeys, d.cnt.p);
   hipLaunchKernelGGL(k_bls_segments, dim3(1), dim3(64), 0, s, d.cnt.p, ks.nkeys, pad, d.seg.p, d.total.p);
-  hipLaunchKernelGGL(k_bls_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, key_idx, n, ks.nkeys, d.seg.p,
+  if (gblocks)
+    hipLaunchKernelGGL(k_bls_scatter, dim3(gblocks), dim3(GROUP_BLOCK), 0, s, key_idx, n, ks.nkeys, d.seg.p,
                      d.cursor.p, d.order.p);
   BLS_HIP(hipGetLastError());
   BLS_HIP(hipEventRecord(d.ev[2], s));
