@@ -754,6 +754,9 @@ def main():
                     help='prepared-key format: auto = wide (radix-256 comb) for node keys (c3), narrow for key pools')
     ap.add_argument('--no-key-cache', action='store_true',
                     help='c3/c4: re-decompress every key per signature instead of preparing each distinct key once')
+    ap.add_argument('--collective', action='store_true',
+                    help='create the process group and run the verdict / quorum all-gathers even at one rank '
+                         '(RCCL exercised on a one-GPU box; the gathered bytes are checked like at N > 1)')
     ap.add_argument('--sequential', action='store_true',
                     help='one stream, each step after the previous one (default: consecutive steps alternate over '
                          'two streams and two workspaces, so step k + 1 starts while step k\'s curve grid drains)')
@@ -778,9 +781,12 @@ def main():
     backend = os.environ.get('PV_BENCH_BACKEND', 'nccl')
     if os.environ.get('PV_BENCH_SHARE_GPU') == '1':
         local = 0
+    # the collectives run when there is more than one rank, or at one rank when
+    # asked (--collective: RCCL initialised and used on a one-GPU lease)
+    coll = world > 1 or args.collective
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
+    if coll:
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
         else:
@@ -817,7 +823,7 @@ def main():
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)] if pipelined else None
     slots = 2 if pipelined else 1
     gathered = [torch.zeros(world * batch.bitmap.numel(), dtype=torch.int64, device=dev)
-                for _ in range(slots)] if world > 1 else None
+                for _ in range(slots)] if coll else None
     tally = None
     if cfg['mode'] == synth.COMMIT:
         nb = n // n_nodes
@@ -834,7 +840,7 @@ def main():
             # timed region, so no step waits on the host (steps stay pipelined)
             tally_device_async(verdict, batch.sender, tally['boff'], n_nodes, tally['q'], tally['votes'][slot],
                                tally['reached'][slot], tally['bad'], streams[slot] if pipelined else None)
-        if world > 1:
+        if coll:
             all_gather(gathered[slot], bitmap)
             if tally is not None:   # C3: batch-sharded tallies, gather the quorum bits
                 all_gather(tally['gathered'][slot], tally['reached'][slot])
@@ -866,7 +872,7 @@ def main():
             batch.verify()
         torch.cuda.synchronize()
         calib_sums = nat.kernel_timing(local, False)
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     # HIP events around each verify launch of the timed steps (sequential
@@ -877,11 +883,11 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if coll:
         t = coll_dev(torch.tensor([elapsed], dtype=torch.float64, device=dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -903,10 +909,10 @@ def main():
             want_votes, want_reached = synth.c3_expected(rank * tally['nb'], tally['nb'], n_nodes, tally['q'])
             mism += int((tally['votes'][slot].cpu().numpy() != want_votes.astype(np.int32)).sum())
             mism += int((tally['reached'][slot].cpu().numpy().astype(bool) != want_reached).sum())
-            if world > 1:
+            if coll:
                 _, all_reached = synth.c3_expected(0, world * tally['nb'], n_nodes, tally['q'])
                 mism += int((tally['gathered'][slot].cpu().numpy().astype(bool) != all_reached).sum())
-        if world > 1:
+        if coll:
             # own slice of the gathered bitmaps == own verdicts, and every rank holds
             # the same gathered bytes (checksums equal under MIN and MAX)
             g = gathered[slot].cpu().numpy()
@@ -920,7 +926,7 @@ def main():
             dist.all_reduce(cks[0], op=dist.ReduceOp.MIN)
             dist.all_reduce(cks[1], op=dist.ReduceOp.MAX)
             mism += int(cks[0].item() != cks[1].item())
-    if world > 1:
+    if coll:
         m = coll_dev(torch.tensor([mism], dtype=torch.int64, device=dev))
         dist.all_reduce(m)
         mism = int(m.item())
@@ -976,7 +982,7 @@ def main():
                        'wide (radix-256 comb)' if batch.wide else 'narrow (radix-16 comb)') if key_cache else 'off', 'tampered': int(tamper.sum()),
                    'parallelism': 'dp{} (disjoint index shards) + {} all-gather of verdict bitmaps'.format(
                        world, 'RCCL' if backend == 'nccl' else backend + ' (rehearsal, ranks share GPU 0)')
-                   if world > 1 else 'single GPU'},
+                   if coll else 'single GPU'},
         'verdict_mismatches': mism,
         'kernel_ms': {'hash': round(ms_hash, 4), 'curve': round(ms_curve, 4), 'timed_on': kernel_ms_on},
         'roofline': {'bound': 'valu', 'kernel': kernel,
@@ -1014,7 +1020,7 @@ def main():
         if TUNED:
             out['tuning'] = dict(TUNED)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if coll:
         dist.barrier()
         dist.destroy_process_group()
     return 0 if mism == 0 else 3

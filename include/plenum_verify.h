@@ -84,6 +84,13 @@ int pv_init(uint32_t device_mask);
 /* Release every device resource.  Safe to call when not initialised. */
 void pv_shutdown(void);
 
+/* TEST ONLY (not part of the node-facing interface): pv_init(0) with k (2..8)
+ * engine devices that all run on HIP device 0, so the multi-device paths of
+ * pv_verify_batch (a worker thread per device, shard offsets, error
+ * aggregation) run on a one-GPU box (tests/test_gpu_multidev.py).  Requires
+ * that no device is initialised (PV_EINVAL otherwise); pv_shutdown ends it. */
+int pv_test_init_dup(uint32_t k);
+
 /* Human-readable description of the last error on this thread ("" if none). */
 const char *pv_last_error(void);
 
@@ -338,11 +345,8 @@ int pv_time_verify_device(const uint8_t *pk, const uint8_t *sig, const uint8_t *
  *                   octet (the shortest chain; takes precedence over
  *                   bls_quad_max).  Default 4096 (0..2^20).
  *   reserved        must be 0.
- *   test_dup_devices  TEST ONLY, read by the next pv_init: 2..8 opens that many
- *                   engine devices, all on HIP device 0, so the multi-device
- *                   paths (a worker thread per device, shard offsets, error
- *                   aggregation) run on a one-GPU box; 0 (default) = one engine
- *                   device per HIP device.
+ * (The test-only duplicate engine devices are not a tuning field: see
+ * pv_test_init_dup below.)
  * pv_get_tuning fills *t with the current values (struct_size must be set to
  * sizeof(pv_tuning) by the caller); pv_set_tuning validates every field
  * (PV_EINVAL and nothing changes if one is out of range), keeps them for later
@@ -370,7 +374,6 @@ typedef struct pv_tuning {
   uint64_t host_ramp;
   uint32_t host_pin_max_mb;
   uint32_t host_trace;
-  uint32_t test_dup_devices;
   uint32_t bls_quad_max;
   uint32_t bls_oct_max;
   uint32_t reserved;
@@ -440,6 +443,18 @@ int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, c
  * device; replaces the previous key set).  status (k bytes, may be NULL) gets
  * PV_BLS_KEY_*.  PV_EINVAL if the generator is not PV_BLS_KEY_OK. */
 int pv_bls_set_keys(const uint8_t *gen, const uint8_t *pks, uint64_t k, uint8_t *status, int device);
+
+/* Append k keys (k x 128 B) to the key set of pv_bls_set_keys on `device`
+ * WITHOUT re-preparing the keys already there: one k_bls_lines launch over the
+ * k new points (a node key added by a NODE txn, bls_key_register).  Their key
+ * indices are *first .. *first + k - 1 (first may be NULL); status as in
+ * pv_bls_set_keys.  PV_ENOTINIT without a set; PV_EINVAL past 65535 keys (the
+ * set is left as it was on any error). */
+int pv_bls_add_keys(const uint8_t *pks, uint64_t k, uint8_t *status, uint64_t *first, int device);
+
+/* The key set on `device`: keys in it and the points k_bls_lines has prepared
+ * for it so far (cumulative over pv_bls_set_keys / pv_bls_add_keys). */
+int pv_bls_keyset_info(int device, uint64_t *nkeys, uint64_t *points_prepared);
 
 /* n checks from HOST memory: check j = (sig[j] 128 B, message msg_idx[j] of
  * msg_blob/msg_off (n_msgs messages, msg_off has n_msgs+1 entries), key

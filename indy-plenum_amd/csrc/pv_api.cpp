@@ -401,7 +401,7 @@ int ws_end(Workspace& w, hipStream_t s) {
 
 struct Device {
   int id = -1;   // engine device id: the device_mask bit and the `device` argument
-  int ord = -1;  // HIP ordinal (== id, except under PV_TEST_DUP_DEVICE)
+  int ord = -1;  // HIP ordinal (== id, except under pv_test_init_dup)
   hipStream_t stream = nullptr;
   hipStream_t copy = nullptr;   // host-buffer calls: H2D of chunk c+1 overlaps the kernels of chunk c
   hipEvent_t copied = nullptr;  // recorded on `copy` after each chunk's inputs, waited on by `stream`
@@ -515,6 +515,7 @@ pv_tuning default_tuning() {
   return t;
 }
 pv_tuning g_tune = default_tuning();
+int g_dup = 0;   // pv_test_init_dup: engine devices sharing HIP device 0 (test only)
 
 int check_tuning(const pv_tuning& t) {
   if (t.struct_size != sizeof(pv_tuning))
@@ -532,7 +533,6 @@ int check_tuning(const pv_tuning& t) {
     return fail(PV_EINVAL, "host_ramp must be 0 or in 1024..2^20");
   if (t.host_pin_max_mb < 16 || t.host_pin_max_mb > 4096) return fail(PV_EINVAL, "host_pin_max_mb must be in 16..4096");
   if (t.host_trace > 1) return fail(PV_EINVAL, "host_trace must be 0 or 1");
-  if (t.test_dup_devices == 1 || t.test_dup_devices > 8) return fail(PV_EINVAL, "test_dup_devices must be 0 or 2..8");
   if (t.bls_quad_max > (1u << 20) || t.bls_oct_max > (1u << 20))
     return fail(PV_EINVAL, "bls_quad_max / bls_oct_max must be <= 2^20");
   if (t.reserved != 0) return fail(PV_EINVAL, "reserved must be 0");
@@ -1259,16 +1259,12 @@ std::vector<Device*> select_devs(uint32_t mask) {
 
 extern "C" {
 
-int pv_init(uint32_t device_mask) {
-  std::lock_guard<std::mutex> lk(g_mu);
+// engine devices 0..dup-1 all on HIP device 0 (pv_test_init_dup), else one per HIP device
+static int init_devices(uint32_t device_mask, int dup) {
   DeviceGuard dg;
   int count = 0;
   hipError_t e = hipGetDeviceCount(&count);
   if (e != hipSuccess || count <= 0) return fail(PV_ENODEV, "no HIP device available (%s)", hipGetErrorString(e));
-  // tuning.test_dup_devices = k (test only, 2..8): k engine devices 0..k-1 all
-  // on HIP device 0, so the multi-device paths (one worker thread per device,
-  // shard offsets, error aggregation) run on a one-GPU box
-  const int dup = (int)g_tune.test_dup_devices;
   const int n_ids = dup ? dup : count;
   for (int id = 0; id < n_ids && id < 32; ++id) {
     if (device_mask && !((device_mask >> id) & 1u)) continue;
@@ -1291,12 +1287,28 @@ int pv_init(uint32_t device_mask) {
   return PV_OK;
 }
 
+int pv_init(uint32_t device_mask) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return init_devices(device_mask, g_dup);
+}
+
+int pv_test_init_dup(uint32_t k) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (k < 2 || k > 8) return fail(PV_EINVAL, "pv_test_init_dup: k must be in 2..8 (got %u)", k);
+  if (!g_devs.empty()) return fail(PV_EINVAL, "pv_test_init_dup: devices already initialised (call pv_shutdown first)");
+  g_dup = (int)k;
+  const int rc = init_devices(0, g_dup);
+  if (rc != PV_OK) g_dup = 0;
+  return rc;
+}
+
 void pv_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceGuard dg;
   for (auto& d : g_devs) release_device(d);
   g_devs.clear();
   g_kc.clear();
+  g_dup = 0;
 }
 
 int pv_keycache_add(const uint8_t* pk, uint64_t k) {
@@ -1664,9 +1676,6 @@ int pv_set_tuning(const pv_tuning* t) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!t) return fail(PV_EINVAL, "null pointer");
   if (int rc = check_tuning(*t)) return rc;
-  const bool dup_changed = t->test_dup_devices != g_tune.test_dup_devices;
-  if (dup_changed && !g_devs.empty())
-    return fail(PV_EINVAL, "test_dup_devices is read by pv_init: call pv_shutdown first");
   g_tune = *t;
   pvbls::set_quad_max(g_tune.bls_quad_max);
   pvbls::set_oct_max(g_tune.bls_oct_max);

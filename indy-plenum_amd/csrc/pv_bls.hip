@@ -565,6 +565,28 @@ struct Buf {
     if (e == hipSuccess) cap = want;
     return e;
   }
+  // grow to >= n elements keeping the first `keep` (device copy on stream s,
+  // synchronised): the incremental key set (pv_bls_add_keys)
+  hipError_t grow_keep(size_t n, size_t keep, hipStream_t s) {
+    if (n <= cap && p) return hipSuccess;
+    size_t want = cap ? cap : 64;
+    while (want < n) want *= 2;
+    T* q = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), want * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (keep && p) {
+      e = hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) {
+        (void)hipFree(q);
+        return e;
+      }
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    cap = want;
+    return hipSuccess;
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -576,10 +598,13 @@ struct Buf {
 // keys (or, for multi-signature checks, the per-check aggregated keys)
 struct KeySet {
   uint32_t nkeys = 0;             // lines of 1 + nkeys points are valid (0: no set)
+  bool gen_ok = false;            // point 0 (the generator) prepared: pv_bls_add_keys may append
+  uint64_t points_prepared = 0;   // points k_bls_lines prepared for this set, cumulative (pv_bls_keyset_info)
   Buf<uint32_t> lines;
   Buf<uint8_t> kstatus, pts;
   void release() {
     nkeys = 0;
+    gen_ok = false;
     lines.release();
     kstatus.release();
     pts.release();
@@ -754,6 +779,7 @@ int pv_bls_set_keys(const uint8_t* gen, const uint8_t* pks, uint64_t k, uint8_t*
   // the old set is gone from here on: a failure below leaves NO set (verify ->
   // PV_ENOTINIT), never a key count over freed or half-written tables
   d->keys.nkeys = 0;
+  d->keys.gen_ok = false;
   BLS_HIP(hipSetDevice(device));
   KeySet& ks = d->keys;
   const uint64_t np = k + 1;
@@ -770,7 +796,56 @@ int pv_bls_set_keys(const uint8_t* gen, const uint8_t* pks, uint64_t k, uint8_t*
   BLS_HIP(hipStreamSynchronize(d->stream));
   if (st[0] != 0) return bfail(PV_EINVAL, "the generator is not a point of order r on the twist (status %d)", st[0]);
   ks.nkeys = (uint32_t)k;
+  ks.gen_ok = true;
+  ks.points_prepared += np;
   if (status) memcpy(status, st.data() + 1, k);
+  return PV_OK;
+}
+
+int pv_bls_add_keys(const uint8_t* pks, uint64_t k, uint8_t* status, uint64_t* first, int device) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  Guard gd;
+  if (k && !pks) return bfail(PV_EINVAL, "null buffer");
+  BlsDev* d = nullptr;
+  if (int rc = bls_dev(device, &d)) return rc;
+  KeySet& ks = d->keys;
+  if (!ks.gen_ok)
+    return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", device);
+  const uint64_t old = ks.nkeys;
+  if (old + k > 65535)
+    return bfail(PV_EINVAL, "at most 65535 keys per set (%llu + %llu)", (unsigned long long)old,
+                 (unsigned long long)k);
+  if (first) *first = old;
+  if (k == 0) return PV_OK;
+  BLS_HIP(hipSetDevice(device));
+  // the prepared points 0..old keep their lines; a failed growth leaves the set as it was
+  const uint64_t np = old + 1 + k;
+  BLS_HIP(ks.pts.grow_keep(np * 128, (old + 1) * 128, d->stream));
+  BLS_HIP(ks.lines.grow_keep(np * KEY_LINE_WORDS, (old + 1) * KEY_LINE_WORDS, d->stream));
+  BLS_HIP(ks.kstatus.grow_keep(np, old + 1, d->stream));
+  BLS_HIP(hipMemcpyAsync(ks.pts.p + 128 * (old + 1), pks, k * 128, hipMemcpyHostToDevice, d->stream));
+  hipLaunchKernelGGL(k_bls_lines, dim3(blocks_for(k, 64)), dim3(64), 0, d->stream, ks.pts.p + 128 * (old + 1),
+                     (uint32_t)k, ks.lines.p + (uint64_t)KEY_LINE_WORDS * (old + 1), ks.kstatus.p + old + 1);
+  BLS_HIP(hipGetLastError());
+  std::vector<uint8_t> st(k);
+  BLS_HIP(hipMemcpyAsync(st.data(), ks.kstatus.p + old + 1, k, hipMemcpyDeviceToHost, d->stream));
+  BLS_HIP(hipStreamSynchronize(d->stream));
+  ks.nkeys = (uint32_t)(old + k);
+  ks.points_prepared += k;
+  if (status) memcpy(status, st.data(), k);
+  return PV_OK;
+}
+
+int pv_bls_keyset_info(int device, uint64_t* nkeys, uint64_t* points_prepared) {
+  std::lock_guard<std::mutex> lk(g_bls_mu);
+  for (auto& d : g_bls)
+    if (d.ord == device) {
+      if (nkeys) *nkeys = d.keys.nkeys;
+      if (points_prepared) *points_prepared = d.keys.points_prepared;
+      return PV_OK;
+    }
+  if (nkeys) *nkeys = 0;
+  if (points_prepared) *points_prepared = 0;
   return PV_OK;
 }
 

@@ -515,6 +515,96 @@ PV_HD void fe_sq2(fe& h0, const fe& f0, fe& h1, const fe& f1) {
   PV_FE_FENCE();
 }
 
+// ---- latency forms (a wave alone on its SIMD: the latency kernels).
+// The carry-seeded columns of fe_mul / fe_sq are ONE dependent chain per
+// product (column k starts from column k-1's carry), which suits the
+// throughput kernels: two waves per SIMD hide each other's latency and every
+// saved instruction counts.  A wave ALONE issues a dependent v_mad_u64_u32
+// every ~10 cycles but independent ones every ~5.5
+// (profiles/r05_lane_exec.json: mad_dep vs mad_ind4).  Here every column
+// starts from zero, two columns' chains are interleaved in one asm block, and
+// the carries run afterwards in the same order -- acc_k = C_k + carry_{k-1},
+// limb_k = acc_k & mask, carry_k = acc_k >> 25/26, then the x19 wrap -- so
+// acc_k, and hence every limb, is bit-identical to fe_mul / fe_sq_t's (the
+// same bounds hold; the host build runs the seeded forms).
+#if defined(PV_MADN_PLAIN)
+PV_HD void fe_mul_l(fe& h, const fe& f, const fe& g) { fe_mul(h, f, g); }
+template <int MULT>
+PV_HD void fe_sq_lt(fe& h, const fe& f) {
+  if (MULT == 1) fe_sq(h, f);
+  else fe_sq2x(h, f);
+}
+#else
+PV_HD void fe_carry_columns(fe& h, const uint64_t col[10]) {
+  uint64_t carry = 0;
+  uint32_t out[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const uint64_t acc = k == 0 ? col[0] : col[k] + carry;
+    carry = acc >> ((k & 1) ? 25 : 26);
+    out[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
+  }
+  fe_finish_columns(h, carry, out);
+}
+PV_HD void fe_mul_l(fe& h, const fe& f, const fe& g) {
+  PV_COUNT(mul);
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int j = 1; j < 10; ++j) g19[j] = 19u * g.v[j];
+#pragma unroll
+  for (int i = 1; i < 10; i += 2) f2[i] = twice(f.v[i]);
+  uint64_t col[10];
+#pragma unroll
+  for (int k = 0; k < 10; k += 2) {
+    uint32_t a[2][10], b[2][10];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+        const int j = (k + c - i + 10) % 10;
+        const bool oo = (i & 1) && (j & 1);
+        a[c][i] = oo ? f2[i] : f.v[i];
+        b[c][i] = i + j >= 10 ? g19[j] : g.v[j];
+      }
+    }
+    madc10x2z(col[k], col[k + 1], a[0], b[0], a[1], b[1]);
+  }
+  fe_carry_columns(h, col);
+  PV_FE_FENCE();
+}
+template <int MULT>
+PV_HD void fe_sq_lt(fe& h, const fe& f) {
+  PV_COUNT(sq);
+  sq_ops o;
+  sq_prepare(o, f);
+  uint64_t col[10];
+  uint32_t as[10][6], bs[10][6];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) sq_column<MULT>(o, k, as[k], bs[k]);
+  // pairs of equal width, in carry order: (0,2) (1,3) (4,6) (5,7) (8,9)
+  madc6x2z(col[0], col[2], as[0], bs[0], as[2], bs[2]);
+  madc5x2z(col[1], col[3], as[1], bs[1], as[3], bs[3]);
+  madc6x2z(col[4], col[6], as[4], bs[4], as[6], bs[6]);
+  madc5x2z(col[5], col[7], as[5], bs[5], as[7], bs[7]);
+  madc6_5z(col[8], col[9], as[8], bs[8], as[9], bs[9]);
+  fe_carry_columns(h, col);
+  PV_FE_FENCE();
+}
+#endif
+PV_HD void fe_sq_l(fe& h, const fe& f) {
+  PV_CHECK_SQ(f);
+  fe_sq_lt<1>(h, f);
+}
+PV_HD void fe_sq2x_l(fe& h, const fe& f) {
+  PV_CHECK_SQ2X(f);
+  fe_sq_lt<2>(h, f);
+}
+PV_HD void fe_sqn_l(fe& h, const fe& f, int n) {
+  fe_sq_l(h, f);
+#pragma unroll 1
+  for (int i = 1; i < n; ++i) fe_sq_l(h, h);
+}
+
 PV_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
 #pragma unroll 1

@@ -24,6 +24,7 @@ _vp = ctypes.c_void_p
 SIGNATURES = [
     ('pv_init', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_shutdown', None, []),
+    ('pv_test_init_dup', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_last_error', ctypes.c_char_p, []),
     ('pv_device_count', ctypes.c_int, []),
     ('pv_verify_batch', ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, ctypes.c_uint32]),
@@ -79,6 +80,9 @@ SIGNATURES = [
     ('pv_keycache_clear', ctypes.c_int, []),
     ('pv_keycache_size', ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     ('pv_bls_set_keys', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    ('pv_bls_add_keys', ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    ('pv_bls_keyset_info', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_uint64)]),
     ('pv_bls_verify_batch', ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     ('pv_bls_verify_batch_device', ctypes.c_int,
@@ -116,8 +120,7 @@ class Tuning(ctypes.Structure):
                 ('host_fused', ctypes.c_uint32), ('host_staging', ctypes.c_uint32), ('host_chunks', ctypes.c_uint32),
                 ('host_first_pct', ctypes.c_uint32), ('host_copy_threads', ctypes.c_uint32),
                 ('host_ramp', ctypes.c_uint64), ('host_pin_max_mb', ctypes.c_uint32), ('host_trace', ctypes.c_uint32),
-                ('test_dup_devices', ctypes.c_uint32), ('bls_quad_max', ctypes.c_uint32),
-                ('bls_oct_max', ctypes.c_uint32), ('reserved', ctypes.c_uint32)]
+                ('bls_quad_max', ctypes.c_uint32), ('bls_oct_max', ctypes.c_uint32), ('reserved', ctypes.c_uint32)]
 
 
 CURVE_MODES = {0: 'half', 1: 'full', 2: 'grouped'}   # PV_CURVE_HALF / _FULL / _GROUPED
@@ -352,6 +355,15 @@ def ensure_init(device_mask=0):
         _inited_mask = 0 if device_mask == 0 else (device_mask | (_inited_mask or 0))
 
 
+def test_init_dup(k):
+    """TEST ONLY: pv_test_init_dup -- k engine devices on HIP device 0 (the
+    multi-device paths on a one-GPU box); nothing may be initialised yet."""
+    global _inited_mask
+    with _lock:
+        _check('pv_test_init_dup', load().pv_test_init_dup(int(k)))
+        _inited_mask = 0
+
+
 def shutdown():
     global _inited_mask
     with _lock:
@@ -475,27 +487,80 @@ def _bls_check(fn, rc):
         raise PlenumGpuError(fn, rc, load().pv_bls_last_error().decode(errors='replace'))
 
 
-_bls_owner = {}   # device -> the object whose key set is on the device
+class _BlsKeySet:
+    """What the device's key set holds (its content, not who asked for it):
+    the generator bytes, key bytes -> index, and each key's status."""
+    __slots__ = ('gen', 'index', 'status')
+
+    def __init__(self, gen):
+        self.gen = gen
+        self.index = {}
+        self.status = []
 
 
-def bls_keyset_owner(device=0):
-    return _bls_owner.get(device)
+_bls_sets = {}   # device -> _BlsKeySet of the set pv_bls_set_keys / pv_bls_add_keys built there
 
 
-def bls_set_keys(gen, pks, device=0, owner=None):
+def bls_set_keys(gen, pks, device=0):
     """pv_bls_set_keys: the generator (128 B) and k keys (k x 128) -> status (k,) u8
     (0 = in G2, 1 = off the twist, 2 = outside the order-r subgroup).  The device
-    holds ONE key set; `owner` records whose it is (bls_keyset_owner)."""
+    holds ONE key set; it replaces whatever was there."""
     ensure_init()
-    _bls_owner[device] = None
+    _bls_sets.pop(device, None)
     gen = np.ascontiguousarray(np.frombuffer(bytes(gen), np.uint8))
     if gen.size != 128:
         raise ValueError('the generator representation is 128 bytes')
     pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(-1, 128)
     st = np.zeros(pks.shape[0], np.uint8)
     _bls_check('pv_bls_set_keys', load().pv_bls_set_keys(_ptr(gen), _ptr(pks), pks.shape[0], _ptr(st), device))
-    _bls_owner[device] = owner
+    ks = _BlsKeySet(gen.tobytes())
+    for i in range(pks.shape[0]):
+        ks.index.setdefault(pks[i].tobytes(), i)
+    ks.status = [int(x) for x in st]
+    _bls_sets[device] = ks
     return st
+
+
+def bls_add_keys(pks, device=0):
+    """pv_bls_add_keys: append k keys (k x 128) to the device's key set without
+    re-preparing it -> (first index, status (k,) u8)."""
+    ensure_init()
+    pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(-1, 128)
+    st = np.zeros(pks.shape[0], np.uint8)
+    first = ctypes.c_uint64()
+    _bls_check('pv_bls_add_keys', load().pv_bls_add_keys(_ptr(pks), pks.shape[0], _ptr(st), ctypes.byref(first),
+                                                         device))
+    return first.value, st
+
+
+def bls_keyset_info(device=0):
+    """(keys in the device's set, points k_bls_lines prepared for it so far)"""
+    n, pts = ctypes.c_uint64(), ctypes.c_uint64()
+    _bls_check('pv_bls_keyset_info', load().pv_bls_keyset_info(device, ctypes.byref(n), ctypes.byref(pts)))
+    return n.value, pts.value
+
+
+def bls_key_indices(gen, pks, device=0):
+    """Indices of 128-byte keys in the device's key set for generator `gen`,
+    keyed by content: keys already there are reused, new ones appended (one
+    k_bls_lines launch for all of them, pv_bls_add_keys); a set built for
+    another generator is replaced.  -> (indices list, status list of the set)."""
+    gen = bytes(gen)
+    with _lock:
+        ks = _bls_sets.get(device)
+    if ks is None or ks.gen != gen:
+        new = list(dict.fromkeys(pks))
+        bls_set_keys(gen, np.frombuffer(b''.join(new), np.uint8) if new else np.zeros((0, 128), np.uint8),
+                     device=device)
+        ks = _bls_sets[device]
+    else:
+        new = [b for b in dict.fromkeys(pks) if b not in ks.index]
+        if new:
+            first, st = bls_add_keys(np.frombuffer(b''.join(new), np.uint8), device=device)
+            for i, b in enumerate(new):
+                ks.index[b] = first + i
+            ks.status.extend(int(x) for x in st)
+    return [ks.index[b] for b in pks], ks.status
 
 
 def bls_verify_arrays(sig, blob, off, msg_idx, key_idx, sig_len=None, device=0):

@@ -39,6 +39,7 @@ GENERATOR = ('3LHpUjiyFC2q2hD7MnwwNmVXiuaFbQx2XkAFJWzswCjgN1utjsCeLzHsKk1nJvFEaS
 CM_BLS_SIG_WRONG = 2          # crypto/bls/bls_bft_replica.py:9
 PPR_BLS_MULTISIG_WRONG = 1    # :8
 REPR_SIZE = 128               # python-ursa's representation size of a G1 / G2 element
+MULTI_MAX = 65535             # checks per pv_bls_verify_multi_batch call
 
 
 class BlsGroupParamsLoaderIndyCrypto:
@@ -176,8 +177,10 @@ class BlsCryptoVerifierGpu:
     """BlsCryptoVerifierIndyCrypto (bls_crypto_indy_crypto.py:68-109): the four
     methods of the reference verifier with the same signatures and None rules,
     plus batch entry points.  Keys are prepared on the device the first time
-    they are seen (pv_bls_set_keys: the generator + every key so far; a pool's
-    node keys are prepared once).
+    they are seen and kept there, keyed by their bytes (pv_bls_add_keys appends
+    only the new ones; verifiers of one generator share the set).  A proof of
+    possession is checked against a per-call key set instead
+    (pv_bls_verify_multi_batch), so keys of rejected NODE txns never join it.
 
     Prefetch seam (CommitIngress, plenum_gpu/commit_ingress.py): `prefetch`
     verifies many (signature, message, key) triples in one GPU pass and keeps
@@ -190,22 +193,14 @@ class BlsCryptoVerifierGpu:
         if self._generator is None:
             raise ValueError('bad BLS group generator')
         self._device = device
-        self._keys = {}          # pk bytes -> index in the device key set
-        self._status = []
+        self._status = []        # status of every key in the device set (after the last _key_indices)
         self._prefetched = {}    # (signature str, message bytes, pk bytes) -> verdict
         self.gpu_calls = 0       # native verify calls made (tests of the prefetch seam)
 
     # -- key set
     def _key_indices(self, pks):
-        new = [b for b in dict.fromkeys(pks) if b not in self._keys]
-        # the device holds one key set: re-prepare when it is not ours any more
-        if new or _native.bls_keyset_owner(self._device) is not self:
-            allk = list(self._keys) + new
-            st = _native.bls_set_keys(self._generator.as_bytes(), np.frombuffer(b''.join(allk), np.uint8),
-                                      device=self._device, owner=self)
-            self._keys = {b: i for i, b in enumerate(allk)}
-            self._status = list(st)
-        return [self._keys[b] for b in pks]
+        idx, self._status = _native.bls_key_indices(self._generator.as_bytes(), pks, device=self._device)
+        return idx
 
     def key_status(self, pk: VerKey) -> int:
         """PV_BLS_KEY_OK / _INFINITY / _NOT_IN_G2 of a key (prepares it)"""
@@ -278,6 +273,10 @@ class BlsCryptoVerifierGpu:
         bool array, entry i == verify_multi_sig(*items[i]); ONE GPU pass (the
         keys of every check summed on the device, lines of each sum, the checks)."""
         out = np.zeros(len(items), bool)
+        if len(items) > MULTI_MAX:           # pv_bls_verify_multi_batch takes at most 65535 checks
+            for s0 in range(0, len(items), MULTI_MAX):
+                out[s0:s0 + MULTI_MAX] = self.verify_multi_sig_batch(items[s0:s0 + MULTI_MAX])
+            return out
         sigs, sig_len, msgs, midx, keys, pk_off, where = [], [], {}, [], [], [0], []
         for i, (signature, message, pks) in enumerate(items):
             if None in pks:                  # :86-88
@@ -338,8 +337,37 @@ class BlsCryptoVerifierGpu:
         PARITY UNPINNED like every BLS verdict here."""
         if key_proof is None or bls_pk is None:
             return False
-        pk = bls_pk.as_bytes()
-        return bool(self._verify_raw([(key_proof.as_bytes(), pk, pk)])[0])
+        return bool(self.verify_key_proofs_batch([(key_proof, bls_pk)])[0])
+
+    def verify_key_proofs_batch(self, items) -> np.ndarray:
+        """items: [(key_proof ProofOfPossession | None, bls_pk VerKey | None)] ->
+        bool array, entry i == verify_key_proof_of_possession(*items[i]).  The
+        keys are checked against a per-call key set (each a one-key "sum",
+        pv_bls_verify_multi_batch): a NODE txn's key joins the verifier's device
+        set only when it signs COMMITs, never because its proof was checked."""
+        out = np.zeros(len(items), bool)
+        rows, where = [], []
+        for i, (key_proof, bls_pk) in enumerate(items):
+            if key_proof is None or bls_pk is None:
+                continue
+            rows.append((key_proof.as_bytes(), bls_pk.as_bytes()))
+            where.append(i)
+        for s0 in range(0, len(rows), MULTI_MAX):
+            part = rows[s0:s0 + MULTI_MAX]
+            msgs, midx = {}, []
+            for _pop, pk in part:
+                midx.append(msgs.setdefault(pk, len(msgs)))
+            blob, off = _native.pack_messages(list(msgs))
+            self.gpu_calls += 1
+            got = _native.bls_verify_multi_arrays(
+                self._generator.as_bytes(), np.frombuffer(b''.join(p[:REPR_SIZE].ljust(REPR_SIZE, b'\0') for p, _ in part),
+                                                          np.uint8),
+                blob, off, np.array(midx, np.uint32),
+                np.frombuffer(b''.join(pk[:REPR_SIZE].ljust(REPR_SIZE, b'\0') for _, pk in part), np.uint8),
+                np.arange(len(part) + 1, dtype=np.uint64), sig_len=np.array([len(p) for p, _ in part], np.uint64),
+                device=self._device)
+            out[np.array(where[s0:s0 + MULTI_MAX])] = got
+        return out
 
     # -- COMMITs
     def validate_commit_batch(self, commits) -> list:

@@ -18,6 +18,7 @@ node's unchanged per-COMMIT path — `_validate_commit` -> `validate_commit` ->
 COMMITs are checked, in what order, and what is reported stay the reference's;
 verdicts no handler consumed are dropped at the end of the pass.
 """
+from functools import partial
 from typing import Callable, Iterable, List, Optional, Tuple
 
 # plenum/common/constants.py:121-122,173,176; plenum/common/types.py:67
@@ -80,6 +81,7 @@ class CommitIngress:
         self.verifier = verifier
         self.commit_items = commit_items
         self.last_pass = {'commits': 0, 'checks': 0, 'verified': 0}
+        self.last_results = []
 
     def collect(self, wrapped: Iterable[Tuple[object, str]]) -> List[tuple]:
         items = []
@@ -103,16 +105,32 @@ class CommitIngress:
         """Drop the verdicts no handler consumed."""
         self.verifier.drop_prefetched()
 
-    def service(self, wrapped: Iterable[Tuple[object, str]], handler: Callable, limit: Optional[int] = None) -> int:
+    def service(self, wrapped: Iterable[Tuple[object, str]], handler: Callable, limit: Optional[int] = None,
+                stasher=None) -> int:
         """The pass: pre-verify, then hand each (commit, sender) to the node's
-        unchanged handler (OrderingService.process_commit) in arrival order."""
+        unchanged handler (OrderingService.process_commit) in arrival order.
+
+        In the reference a COMMIT reaches process_commit only through the
+        ordering service's StashingRouter (ordering_service.py:198 subscribes
+        `partial(stasher._process, process_commit)`), which reads the handler's
+        `(code, reason)` return to stash the COMMIT for later (STASH_VIEW_3PC,
+        STASH_CATCH_UP, STASH_WAITING_FIRST_BATCH_IN_VIEW, ...) or discard it
+        (stashing_router.py:167-185).  Pass that router as `stasher` and each
+        COMMIT takes the same route: `stasher._process(handler, commit, sender)`.
+        A COMMIT stashed here is replayed by the router later, after end_pass(),
+        and its check then runs as its own verify_sig call.  Without `stasher`
+        the handler is called directly (a handler that already routes, e.g. the
+        network bus's `process_incoming`).  `last_results` keeps what each call
+        returned, in order.  Returns the number of COMMITs handed on."""
         wrapped = list(wrapped)
         if limit is not None:
             wrapped = wrapped[:limit]
+        dispatch = handler if stasher is None else partial(stasher._process, handler)
         self.prefetch(wrapped)
+        self.last_results = []
         try:
             for commit, sender in wrapped:
-                handler(commit, sender)
+                self.last_results.append(dispatch(commit, sender))
         finally:
             self.end_pass()
         return len(wrapped)

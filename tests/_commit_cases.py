@@ -74,3 +74,37 @@ class FakeBlsReplica:
 
 def audit_txn(state_roots, ledger_roots):
     return {'txn': {'data': {'stateRoot': state_roots, 'ledgerRoot': ledger_roots}}}
+
+
+# plenum/common/stashing_router.py:11-13, plenum/server/replica_validator_enums.py:6
+DISCARD, PROCESS, STASH = -1, 0, 1
+STASH_VIEW_3PC = 2
+
+
+class MiniStasher:
+    """The part of the reference StashingRouter a COMMIT passes through:
+    _process (stashing_router.py:167-185: None / PROCESS = processed, DISCARD =
+    dropped, any other code = stashed under that code) and process_all_stashed
+    (:117-136, replaying through the subscribed handler)."""
+
+    def __init__(self):
+        self.stashed, self.discarded, self.handler = {}, [], None
+
+    def _process(self, handler, message, *args):
+        self.handler = handler
+        result = handler(message, *args)
+        code, reason = result if result else (None, None)
+        if not code:
+            return True
+        if code == DISCARD:
+            self.discarded.append((message, args, reason))
+            return True
+        self.stashed.setdefault(code, []).append((message, *args))
+        return False
+
+    def process_all_stashed(self, code=None):
+        for c in sorted(self.stashed) if code is None else [code]:
+            data, self.stashed[c] = self.stashed.get(c, []), []
+            for msg_tuple in data:
+                self._process(self.handler, *msg_tuple)
+

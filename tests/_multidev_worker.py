@@ -1,5 +1,5 @@
-"""Child process of tests/test_gpu_multidev.py: pv_tuning.test_dup_devices = 2
-(set before pv_init; test only) opens two engine devices on HIP device 0, so pv_verify_batch with a two-device mask runs
+"""Child process of tests/test_gpu_multidev.py: pv_test_init_dup(2) (test-only
+init entry point) opens two engine devices on HIP device 0, so pv_verify_batch with a two-device mask runs
 its multi-device branch (one worker thread per device, each run_shard on its
 own streams, workspaces and page-locked rings; errors aggregated per shard --
 csrc/pv_api.cpp pv_verify_batch).  Prints one JSON line."""
@@ -16,8 +16,7 @@ sys.path.insert(0, HERE)
 
 def main():
     from plenum_gpu import _native as nat
-    nat.set_tuning(test_dup_devices=2)
-    nat.ensure_init()
+    nat.test_init_dup(2)
     out = {'devices': nat.load().pv_device_count()}
     r = dict(np.load(os.path.join(HERE, 'golden', 'raw_vectors.npz')))
     want = r['verdict'].astype(bool)

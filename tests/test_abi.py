@@ -107,12 +107,12 @@ def test_library_reads_no_environment(native):
     d = native.get_tuning()
     assert d == {'curve_mode': 0, 'lat_max': 32768, 'lat_keyed_max': 8192, 'small_zc_max': 2048, 'lat_kernel': 0,
                  'host_fused': 1, 'host_staging': 0, 'host_chunks': 8, 'host_first_pct': 50, 'host_copy_threads': 8,
-                 'host_ramp': 32768, 'host_pin_max_mb': 512, 'host_trace': 0, 'test_dup_devices': 0,
+                 'host_ramp': 32768, 'host_pin_max_mb': 512, 'host_trace': 0,
                  'bls_quad_max': 32768, 'bls_oct_max': 4096}
     os.environ['PV_CURVE_MODE'] = 'full'        # ignored by the library itself
     try:
         assert native.get_tuning()['curve_mode'] == 0
-        for bad in ({'curve_mode': 3}, {'host_chunks': 0}, {'host_ramp': 5}, {'test_dup_devices': 1},
+        for bad in ({'curve_mode': 3}, {'host_chunks': 0}, {'host_ramp': 5},
                     {'host_pin_max_mb': 8}, {'lat_max': (1 << 20) + 1},
                     {'bls_quad_max': (1 << 20) + 1}, {'bls_oct_max': (1 << 20) + 1}):
             with pytest.raises(native.PlenumGpuError):
@@ -131,3 +131,18 @@ def test_library_reads_no_environment(native):
         assert native.load().pv_get_tuning(ctypes.byref(t)) == -22
     finally:
         del os.environ['PV_CURVE_MODE']
+
+
+def test_tuning_struct_has_no_test_fields(native):
+    """The node-facing pv_tuning carries schedule knobs only:
+    the duplicate-device test mode is its own test-only entry point,
+    pv_test_init_dup, which refuses bad counts before touching a device."""
+    names = [f for f, _ in native.Tuning._fields_]
+    assert not [f for f in names if f.startswith('test') or 'dup' in f], names
+    hdr = open(os.path.join(REPO, 'include', 'plenum_verify.h')).read()
+    body = hdr[hdr.index('typedef struct pv_tuning'):hdr.index('} pv_tuning;')]
+    assert 'test' not in body and 'dup' not in body
+    assert 'int pv_test_init_dup(uint32_t k);' in hdr
+    for bad in (0, 1, 9):
+        assert native.load().pv_test_init_dup(bad) == -22
+

@@ -3,7 +3,7 @@ pre-pass collects for the reference's validate_commit walk, and that the
 unchanged per-COMMIT path is then served from the prefetched verdicts (one
 verifier pass per Looper pass).  The verifier here is a recording stand-in; the
 GPU test (tests/test_gpu_bls_multi.py) runs the same seam on the kernels."""
-from _commit_cases import Commit, FakeBlsReplica, PrePrepare, audit_txn
+from _commit_cases import STASH_VIEW_3PC, Commit, FakeBlsReplica, MiniStasher, PrePrepare, audit_txn
 
 from plenum_gpu.bls import MultiSignatureValue
 from plenum_gpu.commit_ingress import CommitIngress, replica_commit_items
@@ -73,3 +73,37 @@ def test_pass_serves_per_commit_checks_from_one_prefetch():
     # after the pass the verdicts are gone: the same COMMIT goes to the verifier again
     rep.validate_commit(commits[0][0], commits[0][1], pps[1])
     assert v.single == 2
+
+
+def test_pass_routes_commits_through_the_stasher():
+    """in the reference process_commit is reached only through the
+    ordering service's StashingRouter, which stashes a COMMIT whose handler
+    returns (STASH_VIEW_3PC, reason).  With `stasher` the seam takes that route:
+    the future-view COMMITs are stashed, not dropped, and replayed later -- then
+    checked by their own verify_sig calls (the pass's verdicts are gone)."""
+    nn, nb = 4, 3
+    v, rep, pps = _pool(nn, nb)
+    ing = CommitIngress(v, replica_commit_items(rep, lambda view, seq: pps.get(seq)))
+    view = {'no': 0}
+    results = []
+
+    def process_commit(commit, sender):     # ordering_service.py:436-455, _validate -> STASH_VIEW_3PC
+        if commit.viewNo > view['no']:
+            return STASH_VIEW_3PC, 'future view'
+        results.append((commit.ppSeqNo, sender, rep.validate_commit(commit, sender, pps[commit.ppSeqNo])))
+        return None
+
+    commits = [(Commit(0, b % 2, b, {'1': ('bad' if i == 1 else 'good') + '-%d-%d' % (b, i)}), 'N%d:0' % i)
+               for b in range(1, nb + 1) for i in range(nn)]
+    stasher = MiniStasher()
+    assert ing.service(commits, process_commit, stasher=stasher) == len(commits)
+    future = [c for c, _s in commits if c.viewNo == 1]
+    assert len(stasher.stashed[STASH_VIEW_3PC]) == len(future) > 0
+    assert ing.last_results == [c.viewNo == 0 for c, _s in commits]   # stasher._process: True = processed
+    assert len(results) == len(commits) - len(future) and v.single == 0
+    view['no'] = 1
+    stasher.process_all_stashed()
+    assert len(results) == len(commits) and v.single == len(future)
+    assert sorted(results) == sorted((c.ppSeqNo, s, 2 if c.blsSigs['1'].startswith('bad') else None)
+                                     for c, s in commits)
+

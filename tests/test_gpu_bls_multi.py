@@ -226,3 +226,47 @@ def test_commit_ingress_30_batches_one_gpu_pass(pool, nat):
     for c, s in commits[:3]:
         rep.validate_commit(c, s, pps[c.ppSeqNo])
     assert v.gpu_calls - before == 6
+
+
+def test_key_set_grows_one_key_at_a_time(pool, nat):
+    """VERDICT r4 item 7 / ADVICE r4: the device key set is keyed by content and
+    grows incrementally.  25 node keys met one at a time through verify_sig (the
+    COMMIT path) cost one k_bls_lines point each (pv_bls_add_keys), a second
+    verifier of the same generator re-prepares nothing, and proofs of possession
+    of 25 further keys (node_handler.py:207-213) run against per-call key sets:
+    the persistent set does not grow."""
+    from plenum_gpu.bls import ProofOfPossession, VerKey
+    nat.bls_set_keys(pool['gb'], np.zeros((0, 128), np.uint8))
+    n0, p0 = nat.bls_keyset_info()
+    assert n0 == 0
+    v, v2 = _verifier(), _verifier()
+    for i in range(pool['nn']):
+        key = VerKey(pool['pks'][i].tobytes())
+        assert v.verify_sig(_s(pool['sig'][i % pool['nm'], i]), pool['msgs'][i % pool['nm']], key) is True
+        assert nat.bls_keyset_info() == (i + 1, p0 + i + 1)
+        # the same key again, from either verifier: no preparation
+        assert v2.verify_sig(_s(pool['sig'][i % pool['nm'], i]), pool['msgs'][i % pool['nm']], key) is True
+        assert v.verify_sig(_s(pool['sig'][i % pool['nm'], i]), pool['msgs'][(i + 1) % pool['nm']], key) is False
+        assert nat.bls_keyset_info() == (i + 1, p0 + i + 1)
+    # 25 new keys' proofs of possession: per-call sets, the device set unchanged
+    sks = np.frombuffer(b''.join((int.from_bytes(hashlib.sha256(b'pop' + bytes([i])).digest(), 'big') % bn.R)
+                                 .to_bytes(32, 'big') for i in range(25)), np.uint8).reshape(25, 32)
+    pks = nat.bls_pubkeys(pool['gb'], sks)
+    blob, off = nat.pack_messages([pks[i].tobytes() for i in range(25)])
+    idx = np.arange(25, dtype=np.uint32)
+    pops = nat.bls_sign_arrays(sks, blob, off, idx, idx)
+    for i in range(25):
+        assert v.verify_key_proof_of_possession(ProofOfPossession(pops[i].tobytes()), VerKey(pks[i].tobytes())) is True
+        assert v.verify_key_proof_of_possession(ProofOfPossession(pops[(i + 1) % 25].tobytes()),
+                                                VerKey(pks[i].tobytes())) is False
+    assert nat.bls_keyset_info() == (pool['nn'], p0 + pool['nn'])
+    items = [(ProofOfPossession(pops[i].tobytes()), VerKey(pks[(i * 7) % 25].tobytes())) for i in range(25)]
+    assert list(v.verify_key_proofs_batch(items)) == [(i * 7) % 25 == i for i in range(25)]
+    # a set for another generator replaces this one (content, not owner, decides)
+    gq = bytes(nat.bls_pubkeys(pool['gb'], sks[:1])[0])
+    nat.bls_key_indices(gq, [pool['pks'][0].tobytes()])
+    assert nat.bls_keyset_info()[0] == 1
+    key0 = VerKey(pool['pks'][0].tobytes())
+    assert v.verify_sig(_s(pool['sig'][0, 0]), pool['msgs'][0], key0) is True
+    assert nat.bls_keyset_info()[0] == 1
+

@@ -1,5 +1,5 @@
 """The multi-device branch of pv_verify_batch: a fresh child
-process sets pv_tuning.test_dup_devices = 2 (two engine devices on GPU 0), so the
+process calls the test-only pv_test_init_dup(2) (two engine devices on GPU 0), so the
 per-device worker threads, shard offset rebasing and per-shard error
 aggregation run on a one-GPU box (tests/_multidev_worker.py)."""
 import json
