@@ -25,6 +25,13 @@
 #pragma once
 #include "pv_bn254.h"
 
+// the final exponentiation's Fp12-half operations (out of line by default)
+#ifndef PV_FE_CALL
+#define PV_FE_CALL PV_BN_CALL
+#endif
+#ifndef PV_FE_DCALL
+#define PV_FE_DCALL __device__ __noinline__
+#endif
 // member functions (PV_HD may be `static inline` in the host checker)
 #if defined(__HIPCC__)
 #define PV_MD __host__ __device__ __forceinline__
@@ -481,7 +488,7 @@ PV_HD p6 pr_mul_tail(const p6& t, const p2 (&m)[3]) {
   }
   return r;
 }
-PV_BN_CALL p6 pr_mul(const p6& x, const p6& y) {
+PV_FE_CALL p6 pr_mul(const p6& x, const p6& y) {
   p6 t;   // the out-of-line product first: nothing else is live across the call
 #pragma unroll
   for (int j = 0; j < PL; ++j) t.e[j] = f6mul(x.e[j], y.e[j]);
@@ -508,7 +515,7 @@ PV_HD p6 pr_conj(const p6& x) {
 }
 // 1 / x = (a - b w) / (a^2 - v b^2): role 0 squares a, role 1 b; both invert
 // the same Fp6 norm
-PV_BN_CALL p6 pr_inv(const p6& x) {
+PV_FE_CALL p6 pr_inv(const p6& x) {
   p6 sq;
 #pragma unroll
   for (int j = 0; j < PL; ++j) sq.e[j] = f6mul(x.e[j], x.e[j]);
@@ -541,15 +548,15 @@ PV_HD p6 pr_frob_odd(const p6& x, int n, const uint32_t* const (&g)[10]) {
   (void)n;
   return r;
 }
-PV_BN_CALL p6 pr_frob1(const p6& x) {
+PV_FE_CALL p6 pr_frob1(const p6& x) {
   const uint32_t* const g[10] = {G1_1_A, G1_1_B, G1_2_A, G1_2_B, G1_3_A, G1_3_B, G1_4_A, G1_4_B, G1_5_A, G1_5_B};
   return pr_frob_odd(x, 1, g);
 }
-PV_BN_CALL p6 pr_frob3(const p6& x) {
+PV_FE_CALL p6 pr_frob3(const p6& x) {
   const uint32_t* const g[10] = {G3_1_A, G3_1_B, G3_2_A, G3_2_B, G3_3_A, G3_3_B, G3_4_A, G3_4_B, G3_5_A, G3_5_B};
   return pr_frob_odd(x, 3, g);
 }
-PV_BN_CALL p6 pr_frob2(const p6& x) {
+PV_FE_CALL p6 pr_frob2(const p6& x) {
   p6 r;
 #pragma unroll
   for (int j = 0; j < PL; ++j) {
@@ -588,7 +595,7 @@ PV_HD bool pr_is_one(const p6& x) {
 // Every sum is the pair version's (the same integers, so the same limbs).  The
 // host build has no quad: there pmul / pcyc / preduce / pinv are the pair ops.
 #if defined(__HIP_DEVICE_COMPILE__)
-__device__ __noinline__ p6 pr_mul_q(const p6& x, const p6& y) {
+PV_FE_DCALL p6 pr_mul_q(const p6& x, const p6& y) {
   const int h = prole(0);
   const bool g = qrole();
   p6 t;
@@ -608,7 +615,7 @@ __device__ __noinline__ p6 pr_mul_q(const p6& x, const p6& y) {
   return pr_mul_tail(t, m);
 }
 // pr_inv with its two Fp6 products split (the Fp6 inverse runs on both pairs)
-__device__ __noinline__ p6 pr_inv_q(const p6& x) {
+PV_FE_DCALL p6 pr_inv_q(const p6& x) {
   p6 sq;
   sq.e[0] = f6mul_q(x.e[0], x.e[0]);
   const p6 so = pswap(sq);
@@ -674,7 +681,7 @@ __device__ __forceinline__ void mq_reduce(pslot<ST> S) {
 // again between the two quads (orole g)
 // x y: of pair m's five products (its three of t, its m-product ma, and m2) quad
 // g = 0 forms t's first and second and m2, g = 1 t's third, ma and m2
-__device__ __noinline__ p6 pr_mul_o(const p6& x, const p6& y) {
+PV_FE_DCALL p6 pr_mul_o(const p6& x, const p6& y) {
   const int h = prole(0);
   const bool m = qrole(), g = orole();
   const fp6 &xs = x.e[0], &ys = y.e[0];
@@ -701,7 +708,7 @@ __device__ __noinline__ p6 pr_mul_o(const p6& x, const p6& y) {
   }
   return pr_mul_tail(t, mm);
 }
-__device__ __noinline__ p6 pr_inv_o(const p6& x) {
+PV_FE_DCALL p6 pr_inv_o(const p6& x) {
   p6 sq;
   sq.e[0] = f6mul_o4(x.e[0], x.e[0]);
   const p6 so = pswap(sq);

@@ -207,30 +207,29 @@ def keycache_add(keys):
     keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
     if keys.shape[0]:
         _check('pv_keycache_add', load().pv_keycache_add(_ptr(keys), keys.shape[0]))
+        with _lock:
+            _cached_keys.update(keys[i].tobytes() for i in range(keys.shape[0]))
 
 
-_pending_keys = []   # keys registered before / between GPU calls (keycache_defer)
+_pending_keys = {}   # keys registered before / between GPU calls (keycache_defer), insertion-ordered, unique
+_cached_keys = set()  # keys this process has handed to the device cache (tracked here: no library call)
 
 
 def keycache_defer(raw):
     """Queue a 32-byte key for the device key cache; it is added by the next
-    host-buffer verify call (no GPU work here: addIdr may run before pv_init)."""
+    host-buffer verify call.  No GPU work and no library call here (addIdr may
+    run before pv_init, or on the Looper thread while another thread holds the
+    library in a verify call): the cap counts this process's own bookkeeping."""
     global _cache_dropped
     raw = bytes(raw)
     if len(raw) == 32:
         with _lock:
-            if _cached_estimate() + len(_pending_keys) >= KEYCACHE_MAX:
+            if raw in _pending_keys or raw in _cached_keys:
+                return
+            if len(_cached_keys) + len(_pending_keys) >= KEYCACHE_MAX:
                 _cache_dropped += 1          # over the cap: verified uncached
                 return
-            _pending_keys.append(raw)
-
-
-def _cached_estimate():
-    """keys already in the device cache (0 before the engine is initialised)"""
-    if _inited_mask is None or _lib is None:
-        return 0
-    c = ctypes.c_uint64()
-    return c.value if _lib.pv_keycache_size(ctypes.byref(c)) == 0 else 0
+            _pending_keys[raw] = None
 
 
 KEYCACHE_MAX = 1 << 18   # keys queued for the device cache at most (9,344 B each on every device)
@@ -249,6 +248,8 @@ def _flush_keycache():
             _pending_keys.clear()
         try:
             keycache_add(keys)
+            with _lock:
+                _cached_keys.update(keys)
         except PlenumGpuError as e:
             _cache_dropped += len(keys)
             logging.getLogger(__name__).warning('device key cache: %d keys not cached (%s)', len(keys), e)
@@ -257,6 +258,7 @@ def _flush_keycache():
 def keycache_clear():
     with _lock:
         _pending_keys.clear()
+        _cached_keys.clear()
     if _inited_mask is not None:
         _check('pv_keycache_clear', load().pv_keycache_clear())
 
@@ -367,6 +369,7 @@ def test_init_dup(k):
 def shutdown():
     global _inited_mask
     with _lock:
+        _cached_keys.clear()
         if _lib is not None:
             _lib.pv_shutdown()
             _lib.pv_bls_shutdown()

@@ -18,6 +18,7 @@ import subprocess
 
 import pytest
 
+import _isa_hazards
 from conftest import PKG
 
 LLVM = '/opt/rocm/lib/llvm/bin'
@@ -99,3 +100,51 @@ def test_bls_check_kernel_reads_lines_with_vector_loads(disasm):
     for n, body in bodies.items():
         if n.startswith('_ZN2bn'):
             assert not [ln for ln in body if re.search(r'\ss_load_', ln)], n
+
+
+def test_documented_wait_states_hold_in_every_kernel(disasm):
+    """every producer/consumer pair of the ISA's software
+    wait-state rules (tests/_isa_hazards.py: VALU SGPR write -> VMEM / lane
+    select, VALU VGPR write -> DPP / v_readlane / v_permlane, VALU EXEC write ->
+    DPP, wide VMEM store -> overwrite of its data) has its wait states, in
+    compiler code and inside the generated asm chains alike: the scan covers all
+    pairs of the code object, a superset of those with an end inside an asm
+    string.  LDS reads of a just-written VGPR (ds_swizzle exchanges, LDS
+    addresses) are hardware-interlocked and only counted."""
+    bad, counts, lds = _isa_hazards.scan(disasm)
+    documented = [b for b in bad if b[0] in _isa_hazards.REQUIRED]
+    assert not documented, documented[:5]
+    assert counts['valu_vgpr_dpp'] > 100 and counts['store_data_war'] > 100 and counts['valu_vgpr_readlane'] > 10
+    assert lds > 100
+    # the recorded SMEM pattern occurs only where the compiler put it (readfirstlane over
+    # the kernarg pointer), never from an asm chain's carry-out (the round-3 fault's form)
+    war = [b for b in bad if b[0] == 'smem_base_war']
+    assert all('v_readfirstlane_b32' in b[3] for b in war), war
+
+
+SNIPPETS = {
+    'valu_sgpr_vmem': ['v_add_co_u32_e64 v1, s[4:5], v2, v3', 'global_load_dword v6, v[2:3], s[4:5]'],
+    'valu_sgpr_lanesel': ['v_cmp_eq_u32_e64 s[8:9], v1, v2', 'v_readlane_b32 s10, v3, s8'],
+    'valu_vgpr_dpp': ['v_add_u32_e32 v5, v1, v2', 'v_mov_b32_dpp v6, v5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf'],
+    'valu_exec_dpp': ['v_cmpx_eq_u32_e32 v1, v2', 'v_mov_b32_dpp v6, v7 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf'],
+    'valu_vgpr_readlane': ['v_mad_u64_u32 v[4:5], vcc, v1, v2, v[4:5]', 'v_readfirstlane_b32 s3, v4'],
+    'valu_vgpr_permlane': ['v_add_u32_e32 v8, v1, v2', 'v_permlane32_swap_b32 v8, v9'],
+    'store_data_war': ['global_store_dwordx4 v[0:1], v[4:7], off', 'v_mov_b32_e32 v6, 0'],
+}
+
+
+@pytest.mark.parametrize('rule', sorted(SNIPPETS))
+def test_scanner_flags_each_rule_and_accepts_the_padded_form(rule):
+    """each rule on a two-instruction stream: flagged back to back, accepted
+    with exactly the required s_nop in between (s_nop N = N + 1 states)"""
+    need = _isa_hazards.REQUIRED[rule]
+    p, c = SNIPPETS[rule]
+    head = ['0000000000001000 <k>:']
+    bad, counts, _ = _isa_hazards.scan(head + ['\t' + p, '\t' + c])
+    assert [b[0] for b in bad] == [rule] and counts[rule] == 1
+    short = ['\ts_nop {}'.format(need - 2)] if need >= 2 else []
+    bad, _, _ = _isa_hazards.scan(head + ['\t' + p] + short + ['\t' + c])
+    assert [b[0] for b in bad] == [rule]
+    bad, _, _ = _isa_hazards.scan(head + ['\t' + p, '\ts_nop {}'.format(need - 1), '\t' + c])
+    assert not bad
+

@@ -22,7 +22,7 @@ GEN = bytes.fromhex(json.load(open(os.path.join(os.path.dirname(os.path.abspath(
 
 
 def main(sizes):
-    nat.set_tuning(**nat.tuning_from_env())
+    nat.tuning_from_env()   # applies the PV_* knobs that are set (explicit opt-in)
     nk = 25
     sks = np.frombuffer(b''.join((int.from_bytes(hashlib.sha256(b'k' + bytes([i])).digest(), 'big') % R)
                                  .to_bytes(32, 'big') for i in range(nk)), np.uint8).reshape(nk, 32)
