@@ -739,6 +739,43 @@ def main_f3(args):
     return 0 if mism == 0 else 3
 
 
+# the other configs' lines, measured by the default (driver) run itself as short
+# child runs after the C2 line's timed region: (config, steps, warmup)
+OTHER_CONFIGS = (('c3', 10, 2), ('c4', 5, 1), ('c3bls', 3, 1), ('c1', 5, 1), ('f3', 5, 1))
+
+
+def other_configs():
+    """Short runs of C3, C4, C3-BLS, C1 and f3 (each a fresh child process of
+    this script with --no-cpu-baseline, started after the C2 measurement), so the
+    driver's own run records them; the headline `value` stays C2's.  -> {config:
+    the child's line, trimmed to its measurement} or {config: {'error': ...}}."""
+    import subprocess
+    res = {}
+    keep = ('metric', 'value', 'unit', 'steps', 'warmup', 'ms_per_step', 'verdict_mismatches', 'batches_per_s',
+            'quorum_reached', 'kernel_ms', 'small_batch_latency')
+    for name, steps, warm in OTHER_CONFIGS:
+        t0 = time.perf_counter()
+        try:
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), '--config', name, '--steps', str(steps),
+                                '--warmup', str(warm), '--no-cpu-baseline', '--no-e2e'],
+                               capture_output=True, text=True, timeout=300, cwd=REPO)
+            line = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode in (0, 3) and p.stdout.strip() else None
+        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+            res[name] = {'error': repr(e)[:200]}
+            continue
+        if line is None:
+            res[name] = {'error': 'rc {}: {}'.format(p.returncode, p.stderr[-300:])}
+            continue
+        r = {k: line[k] for k in keep if k in line}
+        r['workload'] = (line.get('config') or {}).get('workload')
+        rf = line.get('roofline') or {}
+        if rf:
+            r['roofline'] = {k: rf.get(k) for k in ('kernel', 'achieved', 'peak', 'unit', 'frac', 'traffic')}
+        r['child_wall_s'] = round(time.perf_counter() - t0, 2)
+        res[name] = r
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -757,6 +794,9 @@ def main():
     ap.add_argument('--collective', action='store_true',
                     help='create the process group and run the verdict / quorum all-gathers even at one rank '
                          '(RCCL exercised on a one-GPU box; the gathered bytes are checked like at N > 1)')
+    ap.add_argument('--no-other-configs', action='store_true',
+                    help='c2 at N = 1: skip the short runs of the other configs (C3, C4, C3-BLS, C1, f3) whose '
+                         'lines the default run reports under "other_configs"')
     ap.add_argument('--sequential', action='store_true',
                     help='one stream, each step after the previous one (default: consecutive steps alternate over '
                          'two streams and two workspaces, so step k + 1 starts while step k\'s curve grid drains)')
@@ -1016,6 +1056,9 @@ def main():
         mism += out['end_to_end']['verdict_mismatches']
         out['small_batch_latency'] = small_batch_latency(batch)
         mism += out['small_batch_latency']['verdict_mismatches']
+    if world == 1 and args.config == 'c2' and not args.n and not args.no_other_configs and not args.collective:
+        out['other_configs'] = other_configs()
+        mism += sum(int(r.get('verdict_mismatches') or 0) for r in out['other_configs'].values())
     if rank == 0:
         if TUNED:
             out['tuning'] = dict(TUNED)

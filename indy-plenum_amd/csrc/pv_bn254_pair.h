@@ -32,6 +32,9 @@
 #ifndef PV_FE_DCALL
 #define PV_FE_DCALL __device__ __noinline__
 #endif
+#ifndef PV_FE_F6MUL
+#define PV_FE_F6MUL f6mul
+#endif
 // member functions (PV_HD may be `static inline` in the host checker)
 #if defined(__HIPCC__)
 #define PV_MD __host__ __device__ __forceinline__
@@ -491,7 +494,7 @@ PV_HD p6 pr_mul_tail(const p6& t, const p2 (&m)[3]) {
 PV_FE_CALL p6 pr_mul(const p6& x, const p6& y) {
   p6 t;   // the out-of-line product first: nothing else is live across the call
 #pragma unroll
-  for (int j = 0; j < PL; ++j) t.e[j] = f6mul(x.e[j], y.e[j]);
+  for (int j = 0; j < PL; ++j) t.e[j] = PV_FE_F6MUL(x.e[j], y.e[j]);
   p2 m[3];
   {
     const p6 xo = pswap(x), yo = pswap(y);
@@ -518,14 +521,14 @@ PV_HD p6 pr_conj(const p6& x) {
 PV_FE_CALL p6 pr_inv(const p6& x) {
   p6 sq;
 #pragma unroll
-  for (int j = 0; j < PL; ++j) sq.e[j] = f6mul(x.e[j], x.e[j]);
+  for (int j = 0; j < PL; ++j) sq.e[j] = PV_FE_F6MUL(x.e[j], x.e[j]);
   const p6 so = pswap(sq);
   p6 r;
 #pragma unroll
   for (int j = 0; j < PL; ++j) {
     const int h = prole(j);
     const fp6 d = f6inv(f6sub(f6sel(h, so.e[j], sq.e[j]), f6mulv(f6sel(h, sq.e[j], so.e[j]))));
-    const fp6 m = f6mul(x.e[j], d);
+    const fp6 m = PV_FE_F6MUL(x.e[j], d);
     r.e[j] = f6sel(h, f6neg(m), m);
   }
   return r;

@@ -886,8 +886,8 @@ hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint3
 // mixes cached and uncached keys); else e itself, and the verdict bits also
 // go to the bitmap as the block's byte.
 constexpr int KQ_NR = 41;   // -R cached in add order (Y-X, Y+X, 2dT, 2Z) + decode verdict
-// PV_KEYED_PHASE (timing variants only, wrong verdicts): 1 skips the -R square
-// root (wave 2), 2 the comb (wave 0), 3 the hash (wave 1)
+// PV_KEYED_PHASE (timing variants only, wrong verdicts), a bit mask: 1 skips the
+// -R square root (wave 2), 2 the comb (wave 0), 4 the hash (wave 1)
 #ifndef PV_KEYED_PHASE
 #define PV_KEYED_PHASE 0
 #endif
@@ -920,14 +920,14 @@ __global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __rest
     if (k < 8) {
       uint32_t dig[16];
       bool pre = false;
-      if (serve && PV_KEYED_PHASE != 3) {
+      if (serve && !(PV_KEYED_PHASE & 4)) {
         const uint8_t* a = pk + 32 * (pk_by_key ? (uint64_t)kidx[j] : j);
         pre = hash_one(dig, a, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
       }
       keyed_record(recs + KQ_WORDS * k, pre, dig);
     }
   } else if (wave == 2) {
-    if (serve && PV_KEYED_PHASE != 1) {
+    if (serve && !(PV_KEYED_PHASE & 1)) {
       load8(enc, sig + 64 * j);
       neg_decode_a(st, enc);
     }
@@ -935,17 +935,17 @@ __global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __rest
   const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
   const uint64_t ic = LIST ? list[ec] : ec;
   qfe acc, e_hi, e_lo;
-  if (wave == 0 && PV_KEYED_PHASE != 2) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
+  if (wave == 0 && !(PV_KEYED_PHASE & 2)) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
   __syncthreads();
   const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
   const uint32_t* r = recs + KQ_WORDS * ((t & 63) >> 3);
   if (wave == 0) {
-    if (PV_KEYED_PHASE != 2) q_comb_side(acc, r, side, kt, e_hi, e_lo, q);
+    if (!(PV_KEYED_PHASE & 2)) q_comb_side(acc, r, side, kt, e_hi, e_lo, q);
   } else if (wave == 2 && k < 8) {
     uint32_t* o = negr + KQ_NR * k;
     bool ok = false;
     ge_p3 P;
-    if (serve && PV_KEYED_PHASE != 1) ok = neg_decode_b(P, st, enc) && y_is_canonical(enc);
+    if (serve && !(PV_KEYED_PHASE & 1)) ok = neg_decode_b(P, st, enc) && y_is_canonical(enc);
     else ge_p3_0(P);
     ge_cached c;
     ge_p3_to_cached(c, P);
