@@ -121,6 +121,9 @@ def _mad_peak():
 TUNED = {}   # pv_tuning fields set from PV_* variables (main)
 CURVE_PMC = os.path.join(REPO, 'profiles', 'r04_curve_pmc.json')   # tools/gpu_pmc_r04.sh on the round-4 build
 BLS_PMC = os.path.join(REPO, 'profiles', 'r04_bls_pmc.json')
+# the keyed configs' curve launches (tools/gpu_pmc_r05.sh on the round-5 build)
+KEYED_PMC = {'c3': os.path.join(REPO, 'profiles', 'r05_c3_pmc.json'),
+             'c4': os.path.join(REPO, 'profiles', 'r05_c4_pmc.json')}
 
 
 def _pmc(path, key):
@@ -131,9 +134,14 @@ def _pmc(path, key):
         return None
 
 
-def _traffic_per_launch():
-    """HBM bytes per C2 curve launch from the committed rocprofv3 PMC summary, or None."""
-    return _pmc(CURVE_PMC, 'hbm_bytes_per_launch')
+def _traffic_per_launch(config='c2', n=None):
+    """HBM bytes per curve launch of the config's full-size line from the committed
+    rocprofv3 PMC summary (C2: r04_curve_pmc.json; C3 / C4: the keyed curve launch
+    of r05_c3 / r05_c4_pmc.json, scaled per signature to the line's n), or None."""
+    if config == 'c2':
+        return _pmc(CURVE_PMC, 'hbm_bytes_per_launch') if n == CONFIGS['c2']['n'] else None
+    per = _pmc(KEYED_PMC[config], 'hbm_bytes_per_unit') if config in KEYED_PMC else None
+    return per * n if per and n else None
 
 
 # SURVEY.md 8(d)'s second work term, W_valu, ALGORITHMIC (VERDICT r2 weak #4):
@@ -997,6 +1005,15 @@ def main():
                'deferred_full_length': {'count': deferred, 'fe_mul': W_MUL_FULL, 'fe_sq': W_SQ_FULL,
                                         'mad': W_MAD_FULL}}
     ms_step = elapsed / args.steps * 1e3
+    # HBM bytes of the dominant launch, from the committed PMC profile of the same
+    # line shape (the curve kernel the profile measured)
+    traffic = None
+    if args.config == 'c2' and not key_cache and curve_mode == 'half':
+        traffic = _traffic_per_launch('c2', n)
+    elif args.config == 'c3' and key_cache and batch.wide:
+        traffic = _traffic_per_launch('c3', n)
+    elif args.config == 'c4' and key_cache and not batch.wide:
+        traffic = _traffic_per_launch('c4', n)
     # the dominant kernel is priced on its own HIP-event duration: in the timed
     # steps when they run one after the other; when they are pipelined the
     # launches overlap (a launch's interval includes the other stream's tail),
@@ -1034,7 +1051,7 @@ def main():
                                   'frac': round(achieved_step / peak, 4),
                                   'note': 'curve MAD work per step / per-step time of the timed region (every kernel '
                                           'of the step charged to the curve)'},
-                     'traffic': _traffic_per_launch() if (args.config, n) == ('c2', CONFIGS['c2']['n']) else None,
+                     'traffic': traffic,
                      'work_per_verify': wpv,
                      'combined_issue': _combined_issue(n / (ms_curve * 1e-3), peak)
                      if (args.config, n) == ('c2', CONFIGS['c2']['n']) and curve_mode == 'half' else None},
