@@ -874,49 +874,64 @@ hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint3
 }
 
 // k_verify_quad_keyed: the latency verdict of signatures whose key is
-// prepared (pv_quad.h q_keyed_side).  A block of 192 threads takes 8
-// signatures in three waves: wave 1 (one lane per signature) runs the
-// pre-checks, SHA-512 and h mod L into an LDS record; wave 2 (one lane per
+// prepared (pv_quad.h q_comb_side).  A block of 64 (KQ_CW + 2) threads takes 8
+// signatures: the hash wave (one lane per signature) runs the pre-checks,
+// SHA-512 and h mod L into an LDS record; the root wave (one lane per
 // signature) decodes -R -- the 250-squaring square-root chain, split around the
-// block's first barrier -- and leaves it in cached form in LDS; wave 0 (8 lanes
-// per signature, two lane quads) runs the comb of h and S as soon as the record
-// is there, overlapping the second half of the decode.  After the second
-// barrier side 1 adds -R and side 0 tests the sum for the identity.
+// block's first barrier -- and leaves it in cached form in LDS; the KQ_CW comb
+// waves (16 lanes per signature: KQ_SIDES = 4 lane quads, two comb tables and
+// two base-point chunks each) run the comb of h and S as soon as the record is
+// there, overlapping the second half of the decode.  After the second barrier
+// side 1 adds -R and the four sides' points are summed over two exchanges
+// (shfl_xor 4, then 8): side 0 tests the total for the identity.  One wave
+// per SIMD (four waves): no two paths share an issue port.
+// Round 5: four sides instead of two -- a comb lane's chain 28 (sq + mul) +
+// 2 x 34 mul -> 28 (sq + mul) + 2 x 20 mul + one more exchange level
+// (profiles/r05_keyed_phase_kernel_stats.txt: hash -> comb was the critical path).
 // LIST: signature e of the launch is list[e] (host-buffer calls whose batch
 // mixes cached and uncached keys); else e itself, and the verdict bits also
 // go to the bitmap as the block's byte.
 constexpr int KQ_NR = 41;   // -R cached in add order (Y-X, Y+X, 2dT, 2Z) + decode verdict
+constexpr int KQ_LPS = 4 * KQ_SIDES;   // lanes per signature in the comb waves
+constexpr int KQ_CW = 8 * KQ_LPS / 64;   // comb waves per block (8 signatures)
+constexpr int KQ_THREADS = 64 * (KQ_CW + 2);
+static_assert(KQ_CW >= 1 && 8 * KQ_LPS == 64 * KQ_CW, "comb lanes fill whole waves");
 // PV_KEYED_PHASE (timing variants only, wrong verdicts), a bit mask: 1 skips the
-// -R square root (wave 2), 2 the comb (wave 0), 4 the hash (wave 1)
+// -R square root (root wave), 2 the comb (comb waves), 4 the hash (hash wave)
 #ifndef PV_KEYED_PHASE
 #define PV_KEYED_PHASE 0
 #endif
 template <bool LIST>
-__global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __restrict__ pk, int pk_by_key,
-                                                           const uint8_t* __restrict__ sig,
-                                                           const uint8_t* __restrict__ blob,
-                                                           const uint64_t* __restrict__ off, uint64_t n,
-                                                           const uint32_t* __restrict__ list,
-                                                           const uint32_t* __restrict__ ktab,
-                                                           const uint32_t* __restrict__ kidx,
-                                                           const uint32_t* __restrict__ bw, uint8_t* __restrict__ verdict,
-                                                           uint8_t* __restrict__ bitmap_bytes, uint64_t bitmap_len) {
+__global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t* __restrict__ pk, int pk_by_key,
+                                                                  const uint8_t* __restrict__ sig,
+                                                                  const uint8_t* __restrict__ blob,
+                                                                  const uint64_t* __restrict__ off, uint64_t n,
+                                                                  const uint32_t* __restrict__ list,
+                                                                  const uint32_t* __restrict__ ktab,
+                                                                  const uint32_t* __restrict__ kidx,
+                                                                  const uint32_t* __restrict__ bw,
+                                                                  uint8_t* __restrict__ verdict,
+                                                                  uint8_t* __restrict__ bitmap_bytes,
+                                                                  uint64_t bitmap_len) {
   __shared__ uint32_t recs[8 * KQ_WORDS];
   __shared__ uint32_t negr[8 * KQ_NR];
+  __shared__ uint32_t vbits[KQ_CW];
   const int t = (int)threadIdx.x;
   const int wave = t >> 6;
+  const bool comb = wave < KQ_CW;
   const uint64_t e0 = (uint64_t)blockIdx.x * 8;
-  const int side = (t >> 2) & 1;
+  const int side = (t >> 2) & (KQ_SIDES - 1);
   const QRole q = qrole_of((uint32_t)t & 3u);
-  const uint64_t e = e0 + (uint64_t)((t & 63) >> 3);
-  const int k = (t & 63);                 // waves 1 and 2: lane k < 8 serves signature e0 + k
+  const int cs = comb ? t / KQ_LPS : 0;   // comb waves: the block's signature of this lane
+  const uint64_t e = e0 + (uint64_t)cs;
+  const int k = (t & 63);                 // hash / root wave: lane k < 8 serves signature e0 + k
   const uint64_t ek = e0 + (uint64_t)k;
-  const bool serve = wave != 0 && k < 8 && ek < n;
+  const bool serve = !comb && k < 8 && ek < n;
   uint64_t j = 0;
   if (serve) j = LIST ? list[ek] : ek;
   NegDecode st;
   uint32_t enc[8];
-  if (wave == 1) {
+  if (wave == KQ_CW) {
     if (k < 8) {
       uint32_t dig[16];
       bool pre = false;
@@ -926,7 +941,7 @@ __global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __rest
       }
       keyed_record(recs + KQ_WORDS * k, pre, dig);
     }
-  } else if (wave == 2) {
+  } else if (wave == KQ_CW + 1) {
     if (serve && !(PV_KEYED_PHASE & 1)) {
       load8(enc, sig + 64 * j);
       neg_decode_a(st, enc);
@@ -935,13 +950,13 @@ __global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __rest
   const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
   const uint64_t ic = LIST ? list[ec] : ec;
   qfe acc, e_hi, e_lo;
-  if (wave == 0 && !(PV_KEYED_PHASE & 2)) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
+  if (comb && !(PV_KEYED_PHASE & 2)) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
   __syncthreads();
   const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
-  const uint32_t* r = recs + KQ_WORDS * ((t & 63) >> 3);
-  if (wave == 0) {
+  const uint32_t* r = recs + KQ_WORDS * cs;
+  if (comb) {
     if (!(PV_KEYED_PHASE & 2)) q_comb_side(acc, r, side, kt, e_hi, e_lo, q);
-  } else if (wave == 2 && k < 8) {
+  } else if (wave == KQ_CW + 1 && k < 8) {
     uint32_t* o = negr + KQ_NR * k;
     bool ok = false;
     ge_p3 P;
@@ -959,24 +974,42 @@ __global__ __launch_bounds__(192) void k_verify_quad_keyed(const uint8_t* __rest
     o[40] = ok ? 1u : 0u;
   }
   __syncthreads();
-  if (wave != 0) return;
-  const uint32_t* nr = negr + KQ_NR * ((t & 63) >> 3);
-  qfe eR, x, x1;
-  q_load_cached(eR, nr, false, q);
-  q_keyed_add_negr(acc, eR, side, q);
-  q_to_cached(x, acc, q);
+  if (comb) {
+    const uint32_t* nr = negr + KQ_NR * cs;
+    qfe eR, x, xo;
+    q_load_cached(eR, nr, false, q);
+    q_keyed_add_negr(acc, eR, side, q);
+    // the sides' sum: side s + 1 -> s for even s (xor 4), then side 2 -> 0 (xor 8) ...
 #pragma unroll
-  for (int i = 0; i < 10; ++i) x1.l[0].v[i] = __shfl_xor(x.l[0].v[i], 4, 64);   // side 1 -> side 0
-  const bool id = q_sum_is_identity(acc, x1, q);
-  const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && nr[40] != 0 && id;
-  const bool mine = side == 0 && (t & 3) == 0 && e < n;
-  if (mine) verdict[ic] = v ? 1 : 0;
+    for (int step = 1; step < KQ_SIDES / 2; step <<= 1) {
+      q_to_cached(x, acc, q);
+#pragma unroll
+      for (int i = 0; i < 10; ++i) xo.l[0].v[i] = __shfl_xor(x.l[0].v[i], 4 * step, 64);
+      q_add(acc, xo, false, q);   // meaningful on sides s % (2 step) == 0; the others compute alike, unused
+    }
+    q_to_cached(x, acc, q);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) xo.l[0].v[i] = __shfl_xor(x.l[0].v[i], 2 * KQ_SIDES, 64);   // side S/2 -> 0
+    const bool id = q_sum_is_identity(acc, xo, q);
+    const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && nr[40] != 0 && id;
+    const bool mine = side == 0 && (t & 3) == 0 && e < n;
+    if (mine) verdict[ic] = v ? 1 : 0;
+    if constexpr (!LIST) {
+      const uint64_t ball = __ballot(mine && v);   // bit KQ_LPS m: signature 64 wave / KQ_LPS + m
+      if ((t & 63) == 0) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int m = 0; m < 64 / KQ_LPS; ++m) bits |= (uint32_t)((ball >> (KQ_LPS * m)) & 1ull) << m;
+        vbits[wave] = bits;
+      }
+    }
+  }
   if constexpr (!LIST) {
-    const uint64_t ball = __ballot(mine && v);   // bits 8k: signature e0 + k
+    __syncthreads();   // every wave (the hash and root waves too): the comb waves' bits are in LDS
     if (t == 0 && bitmap_bytes) {
       uint32_t bits = 0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) bits |= (uint32_t)((ball >> (8 * i)) & 1ull) << i;
+      for (int w = 0; w < KQ_CW; ++w) bits |= vbits[w] << (w * (64 / KQ_LPS));
       bitmap_bytes[blockIdx.x] = (uint8_t)bits;
       if ((uint64_t)blockIdx.x + 1 == gridDim.x)
         for (uint64_t b = (uint64_t)blockIdx.x + 1; b < bitmap_len; ++b) bitmap_bytes[b] = 0;
@@ -994,11 +1027,12 @@ hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uin
   if (list && bitmap) return hipErrorInvalidValue;
   const uint64_t bytes = (n + 63) / 64 * 8;
   if (list)
-    hipLaunchKernelGGL(k_verify_quad_keyed<true>, dim3((uint32_t)blocks), dim3(192), 0, s, pk, pk_by_key ? 1 : 0, sig,
-                       blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0);
+    hipLaunchKernelGGL(k_verify_quad_keyed<true>, dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
+                       pk_by_key ? 1 : 0, sig, blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0);
   else
-    hipLaunchKernelGGL(k_verify_quad_keyed<false>, dim3((uint32_t)blocks), dim3(192), 0, s, pk, pk_by_key ? 1 : 0,
-                       sig, blob, off, n, nullptr, ktab, kidx, bw, verdict, reinterpret_cast<uint8_t*>(bitmap), bytes);
+    hipLaunchKernelGGL(k_verify_quad_keyed<false>, dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
+                       pk_by_key ? 1 : 0, sig, blob, off, n, nullptr, ktab, kidx, bw, verdict,
+                       reinterpret_cast<uint8_t*>(bitmap), bytes);
   return hipGetLastError();
 }
 

@@ -409,15 +409,20 @@ PV_HD bool q_sum_is_identity(const qfe& Q0, const qfe& e1, const QRole& q) {
 // (k_verify_quad_keyed): -A is never decompressed.  The key's 8-way comb
 // tables (key_prepare: k 2^(32 q) (-A), affine niels) and the radix-2^16
 // chunk tables of B give R' = h(-A) + S B in 28 doublings and 80 affine adds
-// (double_scalarmult_comb's schedule), split over the signature's two quads:
-// side s adds the key tables and the base-point chunks q = 4s .. 4s + 3, so a
-// lane runs 28 (sq + mul) + 40 x 2 mul.  libsodium accepts iff encode(R') ==
-// R, i.e. iff R decodes with a canonical y and R' + (-R) = O (the identity
-// test of the half-size path, pv_lattice.h): -R is decoded while the scalar
-// wave hashes, side 1 adds it, and side 0 tests Q0 + Q1 = O.
+// (double_scalarmult_comb's schedule), split over the signature's KQ_SIDES
+// lane quads: side s adds the key tables and the base-point chunks
+// q = (8 / KQ_SIDES) s ..  + 8 / KQ_SIDES - 1, so with four sides a lane runs
+// 28 (sq + mul) + 20 x 2 mul (two sides: 28 (sq + mul) + 40 x 2 mul).  The
+// sides' points are then summed over a tree of exchanges (the kernel's
+// shfl_xor 4 and 8; hc_verify_keyed_quad on the host).  libsodium accepts iff
+// encode(R') == R, i.e. iff R decodes with a canonical y and R' + (-R) = O (the
+// identity test of the half-size path, pv_lattice.h): -R is decoded while the
+// scalar wave hashes, side 1 adds it, and side 0 tests the total for O.
 //
 // record (LDS): h + the radix-16 digit offsets (8 words), pre-check verdict
 constexpr int KQ_H = 0, KQ_OK = 8, KQ_WORDS = 9;
+constexpr int KQ_SIDES = 4;   // lane quads per signature in k_verify_quad_keyed
+constexpr int KQ_TPS = 8 / KQ_SIDES;   // comb tables (and base-point chunks) per side
 
 PV_HD void keyed_record(uint32_t* rec, bool pre, const uint32_t dig[16]) {
   uint32_t hh[8];
@@ -434,7 +439,7 @@ PV_HD void keyed_record(uint32_t* rec, bool pre, const uint32_t dig[16]) {
 }
 
 // S's share of the comb, which needs no hash: with the signed radix-2^16
-// digits of S (offset form), side s sums its chunks q = 4s .. 4s + 3 of the
+// digits of S (offset form), side s sums its chunks q = KQ_TPS s .. of the
 // high halves (added at window 4, i.e. doubled 16 times) and of the low halves
 // (added last) into two points, returned in cached add order.  Runs while the
 // scalar wave hashes.
@@ -442,11 +447,11 @@ PV_HD void q_comb_base(qfe& e_hi, qfe& e_lo, const uint8_t* sig, int side, const
   uint32_t sp[8];
   load8(sp, sig + 32);
   sc_add_pattern(sp, sp, HALF_S_PATTERN);
-  const uint32_t* bws = bw + (uint64_t)(4 * side) * BW_TABLE;
-  qfe ph, pl, eh[4], el[4];
+  const uint32_t* bws = bw + (uint64_t)(KQ_TPS * side) * BW_TABLE;
+  qfe ph, pl, eh[KQ_TPS], el[KQ_TPS];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t wd = pick8(sp, 4 * side + k);
+  for (int k = 0; k < KQ_TPS; ++k) {
+    const uint32_t wd = pick8(sp, KQ_TPS * side + k);
     const int dh = (int)(wd >> 16) - 32768, dl = (int)(wd & 0xffffu) - 32768;
     const uint32_t* t = bws + (uint64_t)k * BW_TABLE;
     q_load_niels(eh[k], t + (uint64_t)(dh < 0 ? -dh : dh) * BT_WORDS, dh < 0, q);
@@ -458,8 +463,8 @@ PV_HD void q_comb_base(qfe& e_hi, qfe& e_lo, const uint8_t* sig, int side, const
     role_p3_identity(pl.l[j], qrole(j, q));
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t wd = pick8(sp, 4 * side + k);
+  for (int k = 0; k < KQ_TPS; ++k) {
+    const uint32_t wd = pick8(sp, KQ_TPS * side + k);
     q_add(ph, eh[k], (wd >> 16) < 32768u, q);
     q_add(pl, el[k], (wd & 0xffffu) < 32768u, q);
   }
@@ -467,24 +472,24 @@ PV_HD void q_comb_base(qfe& e_hi, qfe& e_lo, const uint8_t* sig, int side, const
   q_to_cached(e_lo, pl, q);
 }
 
-// h's share of the comb on side s: the key tables q = 4s .. 4s + 3 (kt = the
+// h's share of the comb on side s: the key tables q = KQ_TPS s .. (kt = the
 // key's 8 comb tables), 8 windows of 4 doublings; the base-point sums of
 // q_comb_base join at window 4 (e_hi) and after the last window (e_lo).  Each
-// window's 4 key entries are fetched before its doublings.
+// window's key entries are fetched before its doublings.
 PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* kt, const qfe& e_hi, const qfe& e_lo,
                        const QRole& q) {
-  uint32_t hp[4];
+  uint32_t hp[KQ_TPS];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) hp[k] = rec[KQ_H + 4 * side + k];
-  const uint32_t* kts = kt + 4 * side * KT_TABLE;
+  for (int k = 0; k < KQ_TPS; ++k) hp[k] = rec[KQ_H + KQ_TPS * side + k];
+  const uint32_t* kts = kt + KQ_TPS * side * KT_TABLE;
 #pragma unroll
   for (int j = 0; j < QL; ++j) role_p3_identity(acc.l[j], qrole(j, q));
 #pragma unroll 1
   for (int w = 7; w >= 0; --w) {
-    qfe ek[4];
-    int dk[4];
+    qfe ek[KQ_TPS];
+    int dk[KQ_TPS];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < KQ_TPS; ++k) {
       dk[k] = (int)((hp[k] >> (4 * w)) & 15u) - 8;
       q_load_niels(ek[k], kts + k * KT_TABLE + (dk[k] < 0 ? -dk[k] : dk[k]) * KT_ENTRY, dk[k] < 0, q);
     }
@@ -493,16 +498,16 @@ PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* 
       for (int k = 0; k < 4; ++k) q_dbl(acc, q);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) q_add(acc, ek[k], dk[k] < 0, q);
+    for (int k = 0; k < KQ_TPS; ++k) q_add(acc, ek[k], dk[k] < 0, q);
     if (w == 4) q_add(acc, e_hi, false, q);
   }
   q_add(acc, e_lo, false, q);
 }
 
-// side 1 adds -R (eR: -R in cached add order, q_load_cached); side 0 adds
-// the identity: the same instruction stream on both quads
+// side 1 adds -R (eR: -R in cached add order, q_load_cached); the other sides
+// add the identity: the same instruction stream on every quad
 PV_HD void q_keyed_add_negr(qfe& acc, const qfe& eR, int side, const QRole& q) {
-  const uint32_t sm = 0u - (uint32_t)(side != 0);
+  const uint32_t sm = 0u - (uint32_t)(side == 1);
   qfe e;
 #pragma unroll
   for (int j = 0; j < QL; ++j) {

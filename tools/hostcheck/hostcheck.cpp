@@ -305,8 +305,10 @@ void hc_verify_keyed_wide(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
   free(pre);
 }
 
-// keyed latency kernel (k_verify_quad_keyed): prepared keys, each side's
-// comb share on an emulated quad, -R added on side 1, identity test
+// keyed latency kernel (k_verify_quad_keyed): prepared keys, each of the
+// KQ_SIDES sides' comb share on an emulated quad, -R added on side 1, the
+// sides summed over the kernel's exchange tree (1 -> 0 and 3 -> 2, then 2 -> 0),
+// identity test on side 0
 void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
                           const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* verdict) {
   ensure_btab();
@@ -321,18 +323,22 @@ void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
     keyed_record(rec, pre, dig);
     uint32_t nr[41];
     keyed_neg_r(nr, sig + 64 * i);
-    qfe eR, Q0, Q1, x1;
+    qfe eR, Q[KQ_SIDES], x;
     q_load_cached(eR, nr, false, qr);
     const uint32_t* kt = ktab + (uint64_t)kidx[i] * KEY_WORDS;
-    qfe h0, l0, h1, l1;
-    q_comb_base(h0, l0, sig + 64 * i, 0, g_bw, qr);
-    q_comb_base(h1, l1, sig + 64 * i, 1, g_bw, qr);
-    q_comb_side(Q0, rec, 0, kt, h0, l0, qr);
-    q_comb_side(Q1, rec, 1, kt, h1, l1, qr);
-    q_keyed_add_negr(Q0, eR, 0, qr);
-    q_keyed_add_negr(Q1, eR, 1, qr);
-    q_to_cached(x1, Q1, qr);
-    verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && nr[40] && q_sum_is_identity(Q0, x1, qr)) ? 1 : 0;
+    for (int s = 0; s < KQ_SIDES; ++s) {
+      qfe hs, ls;
+      q_comb_base(hs, ls, sig + 64 * i, s, g_bw, qr);
+      q_comb_side(Q[s], rec, s, kt, hs, ls, qr);
+      q_keyed_add_negr(Q[s], eR, s, qr);
+    }
+    for (int step = 1; step < KQ_SIDES / 2; step <<= 1)   // the kernel's shfl_xor 4 (step 1), 8 (step 2) ...
+      for (int s = 0; s < KQ_SIDES; s += 2 * step) {
+        q_to_cached(x, Q[s + step], qr);
+        q_add(Q[s], x, false, qr);
+      }
+    q_to_cached(x, Q[KQ_SIDES / 2], qr);
+    verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && nr[40] && q_sum_is_identity(Q[0], x, qr)) ? 1 : 0;
   }
   free(ktab);
 }
