@@ -420,6 +420,8 @@ struct Device {
   uint64_t lat_keyed_max = PV_LAT_KEYED_MAX;  // keyed batches up to this size: k_verify_quad_keyed
   uint64_t zc_max = PV_SMALL_ZC_MAX;          // host calls up to this size: zero-copy (tuning.small_zc_max)
   PinBuf zc_in, zc_out;                       // fine-grained page-locked image / verdicts of zero-copy calls
+  PinBuf zc_flag;                             // completion word of zero-copy calls (k_signal), polled by the host
+  uint32_t zc_seq = 0;
   bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_PAIR: k_curve_lat
   // host-buffer chunks of generic batches: one k_chunk_half launch per chunk
   // + one k_verify_quad_list pass for the deferred records; tuning.host_fused 0:
@@ -577,7 +579,7 @@ int init_device(Device& d) {
   HIP_OK(hipEventCreateWithFlags(&d.keys_ready, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&d.joined, hipEventDisableTiming));
   for (auto& w : d.ws) HIP_OK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
-  d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped;
+  d.zc_in.flags = d.zc_out.flags = d.zc_flag.flags = hipHostMallocCoherent | hipHostMallocMapped;
   apply_tuning(d, g_tune);
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d.ord));
@@ -659,6 +661,7 @@ void release_device(Device& d) {
   d.pin[1].release();
   d.zc_in.release();
   d.zc_out.release();
+  d.zc_flag.release();
   d.vout.release();
   if (d.pool) d.pool->shutdown();
   d.copy = nullptr;
@@ -871,13 +874,31 @@ uint64_t small_bytes(const HostBatch& hb, uint64_t s, uint64_t e) {
   return (m + 1) * 8 + m * 96 + (hb.off[e] - hb.off[s]) + 16 + 16 + 8 * m;
 }
 
+// PV_ZC_POLL = 0 builds the stream-synchronize completion (A/B variant)
+#ifndef PV_ZC_POLL
+#define PV_ZC_POLL 1
+#endif
+// spins until *w == v (acquire) or `ns` nanoseconds have passed
+constexpr int64_t ZC_SPIN_NS = 20'000'000;
+bool spin_wait_word(const uint32_t* w, uint32_t v, int64_t ns) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == v) return true;
+    if ((i & 255u) == 255u &&
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > ns)
+      return false;
+  }
+}
+
 int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   const uint64_t m = e - s;
   HIP_OK(hipSetDevice(d.ord));
   Workspace& w = d.ws[0];
   struct Drain {
     Device& d;
+    bool done = false;   // the call's work is known complete (zero-copy completion word)
     ~Drain() {
+      if (done) return;
       (void)hipSetDevice(d.ord);
       (void)hipStreamSynchronize(d.ws[0].stream);
     }
@@ -957,8 +978,23 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
                                   vdst, nullptr, w.stream, false, nullptr, nullptr);
     if (rc) return rc;
   }
-  if (!zc) HIP_OK(hipMemcpyAsync(vout.p, d.verdict.p, m, hipMemcpyDeviceToHost, w.stream));
-  HIP_OK(hipStreamSynchronize(w.stream));
+  if (zc && PV_ZC_POLL) {
+    // completion by polling a word k_signal writes after the verify kernels:
+    // ~5 us below a stream synchronize per call (profiles/r05_keyed4_phase_and_sync.jsonl,
+    // tools/ubench/sync_lat.hip); past the spin budget (a fault, a long queue)
+    // the synchronize reports / waits as before
+    HIP_OK(d.zc_flag.ensure(64));
+    void* fp = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&fp, d.zc_flag.p, 0));
+    if (++d.zc_seq == 0) d.zc_seq = 1;
+    const uint32_t seq = d.zc_seq;
+    HIP_OK(pv::launch_signal(static_cast<uint32_t*>(fp), seq, w.stream));
+    drain.done = spin_wait_word(reinterpret_cast<const uint32_t*>(d.zc_flag.p), seq, ZC_SPIN_NS);
+    if (!drain.done) HIP_OK(hipStreamSynchronize(w.stream));
+  } else {
+    if (!zc) HIP_OK(hipMemcpyAsync(vout.p, d.verdict.p, m, hipMemcpyDeviceToHost, w.stream));
+    HIP_OK(hipStreamSynchronize(w.stream));
+  }
   memcpy(hb.verdict + s, vout.p, m);
   return PV_OK;
 }

@@ -126,6 +126,11 @@ hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uin
                                     const uint32_t* kidx, const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap,
                                     hipStream_t s);
 
+// completion signal of a zero-copy host call: *flag = seq (system scope, after
+// every earlier kernel of the stream), polled by the host instead of a stream
+// synchronize (run_small)
+hipError_t launch_signal(uint32_t* flag, uint32_t seq, hipStream_t s);
+
 // keygen + sign: pk[i], sig[i] for seed[i] over M_i
 hipError_t launch_sign(const uint8_t* seeds, const uint8_t* blob, const uint64_t* off, uint64_t n,
                        const uint32_t* btab, uint8_t* pk_out, uint8_t* sig_out, hipStream_t s);

@@ -1036,6 +1036,18 @@ hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uin
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(64) void k_signal(uint32_t* __restrict__ flag, uint32_t seq) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(flag + threadIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t launch_signal(uint32_t* flag, uint32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, s, flag, seq);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------- batch signer
 __global__ __launch_bounds__(256) void k_sign(const uint8_t* __restrict__ seeds, const uint8_t* __restrict__ blob,
                                                const uint64_t* __restrict__ off, uint64_t n,
