@@ -527,6 +527,10 @@ PV_HD void fe_sq2(fe& h0, const fe& f0, fe& h1, const fe& f1) {
 // limb_k = acc_k & mask, carry_k = acc_k >> 25/26, then the x19 wrap -- so
 // acc_k, and hence every limb, is bit-identical to fe_mul / fe_sq_t's (the
 // same bounds hold; the host build runs the seeded forms).
+// MEASURED SLOWER on a lone wave (profiles/r05_fe_lat.json: fe_sq_l 506 vs
+// fe_sq 454 cycles, fe_mul_l 671 vs 654 -- the split columns issue more
+// instructions, and a lone wave is issue-bound): no
+// kernel uses them; tools/ubench/fe_lat.hip keeps the comparison reproducible.
 #if defined(PV_MADN_PLAIN)
 PV_HD void fe_mul_l(fe& h, const fe& f, const fe& g) { fe_mul(h, f, g); }
 template <int MULT>
