@@ -119,7 +119,7 @@ def _mad_peak():
 
 
 TUNED = {}   # pv_tuning fields set from PV_* variables (main)
-CURVE_PMC = os.path.join(REPO, 'profiles', 'r04_curve_pmc.json')   # tools/gpu_pmc_r04.sh on the round-4 build
+CURVE_PMC = os.path.join(REPO, 'profiles', 'r05_curve_pmc.json')   # tools/gpu_final_r05.sh on the round-5 build
 BLS_PMC = os.path.join(REPO, 'profiles', 'r04_bls_pmc.json')
 # the keyed configs' curve launches (tools/gpu_pmc_r05.sh on the round-5 build)
 KEYED_PMC = {'c3': os.path.join(REPO, 'profiles', 'r05_c3_pmc.json'),
@@ -136,7 +136,7 @@ def _pmc(path, key):
 
 def _traffic_per_launch(config='c2', n=None):
     """HBM bytes per curve launch of the config's full-size line from the committed
-    rocprofv3 PMC summary (C2: r04_curve_pmc.json; C3 / C4: the keyed curve launch
+    rocprofv3 PMC summary (C2: r05_curve_pmc.json; C3 / C4: the keyed curve launch
     of r05_c3 / r05_c4_pmc.json, scaled per signature to the line's n), or None."""
     if config == 'c2':
         return _pmc(CURVE_PMC, 'hbm_bytes_per_launch') if n == CONFIGS['c2']['n'] else None
@@ -190,7 +190,7 @@ def _combined_issue(kernel_rate, peak):
     (constants above, pinned by host op counts) and every P measured (the MAD
     ceiling; the other two classes at their measured ratios to it).  Beside it,
     `issue_efficiency` prices the instructions the kernel actually EXECUTES
-    (rocprofv3 SQ_INSTS_VALU, profiles/r04_curve_pmc.json) the same way."""
+    (rocprofv3 SQ_INSTS_VALU, profiles/r05_curve_pmc.json) the same way."""
     try:
         p_half, p_full = _class_rates(peak)
     except (OSError, KeyError, ValueError):
@@ -216,7 +216,7 @@ def _combined_issue(kernel_rate, peak):
         rate_exec = 1.0 / (W_MAD_PER_VERIFY / peak + other / p_half)
         out['issue_efficiency'] = {'executed_non_mad_per_verify': round(other), 'rate_at_executed_work': round(rate_exec, 1),
                                    'frac': round(kernel_rate / rate_exec, 4),
-                                   'source': 'rocprofv3 SQ_INSTS_VALU of the C2 curve launch (profiles/r04_curve_pmc.json)'}
+                                   'source': 'rocprofv3 SQ_INSTS_VALU of the C2 curve launch (profiles/r05_curve_pmc.json)'}
     except (OSError, KeyError, ValueError):
         pass
     return out
@@ -795,6 +795,8 @@ def main():
                     help='signatures per GPU (default: the config\'s); spell it --count under torch.distributed.run')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true', help='skip the host-buffer (PCIe-inclusive) measurement')
+    ap.add_argument('--key-mod', type=int, default=None,
+                    help='experiment: override the config key pool size (keys = i mod N; the line records it)')
     ap.add_argument('--key-format', choices=('auto', 'narrow', 'wide'), default='auto',
                     help='prepared-key format: auto = wide (radix-256 comb) for node keys (c3), narrow for key pools')
     ap.add_argument('--no-key-cache', action='store_true',
@@ -851,7 +853,9 @@ def main():
             dist.all_gather_into_tensor(o, inp.cpu())
             out.copy_(o)
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.key_mod is not None:
+        cfg['key_mod'] = args.key_mod
     n = args.n or cfg['n']
     n_nodes = cfg.get('n_nodes', 25)
     if cfg['mode'] == synth.COMMIT:
