@@ -148,22 +148,15 @@ PV_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q, bool neg) {
 // Restates ge25519_frombytes_negate_vartime's contract (SURVEY.md App. C.2
 // step 4): fails iff (y^2-1)/(dy^2+1) has no square root; x == 0 with the
 // sign bit set is accepted (libsodium 1.0.18).
-// -P from its encoding in two phases (the keyed latency kernel runs them on
-// either side of a block barrier): phase a forms y, u = y^2 - 1, v = d y^2 + 1,
-// z = u v^7 and z's (p-5)/8 power chain up to z^(2^50-1), z^(2^100-1) and
-// PV_ROOT_PRE_SQ of the 100 squarings towards z^(2^200-1); phase b finishes
-// the chain and the square-root checks.  The operations and their order are
-// exactly fe_pow22523's.  The split point is a timing knob of the keyed latency
-// kernel, whose root wave meets the hash wave at the barrier between the
-// phases: moving squarings before it measured slower (kernel 84.6 / 88.9 / 95.6
-// us at 0 / 30 / 60 extra squarings, profiles/r05_root_split.jsonl), so the
-// default keeps the round-3 split.
-#ifndef PV_ROOT_PRE_SQ
-#define PV_ROOT_PRE_SQ 0
-#endif
-static_assert(PV_ROOT_PRE_SQ >= 0 && PV_ROOT_PRE_SQ < 100, "split inside the 2^200 step");
+// -P from its encoding in two phases: phase a forms y, u = y^2 - 1,
+// v = d y^2 + 1, z = u v^7 and the first half of z's (p-5)/8 power chain
+// (z^(2^50-1), z^(2^100-1)); phase b finishes the chain and the square-root
+// checks.  The operations and their order are exactly fe_pow22523's.  (Rounds
+// 3-4 ran the phases on either side of a block barrier in the keyed latency
+// kernel; round 5 measured moving the split (profiles/r05_root_split.jsonl) and
+// then replaced the barrier by LDS flags, so the chain now runs in one piece.)
 struct NegDecode {
-  fe Y, u, v, v3, z, a, b, t;
+  fe Y, u, v, v3, z, a, b;
 };
 
 PV_HD void neg_decode_a(NegDecode& st, const uint32_t s[8]) {
@@ -193,14 +186,11 @@ PV_HD void neg_decode_a(NegDecode& st, const uint32_t s[8]) {
   fe_sqn(t, c, 20);     fe_mul(t, t, c);        // 2^40 - 1
   fe_sqn(t, t, 10);     fe_mul(st.a, t, st.b);  // 2^50 - 1
   fe_sqn(t, st.a, 50);  fe_mul(st.b, t, st.a);  // 2^100 - 1
-  if (PV_ROOT_PRE_SQ > 0) fe_sqn(st.t, st.b, PV_ROOT_PRE_SQ);
-  else fe_copy(st.t, st.b);
 }
 
 PV_HD bool neg_decode_b(ge_p3& h, NegDecode& st, const uint32_t s[8]) {
   fe t;
-  fe_sqn(t, st.t, 100 - PV_ROOT_PRE_SQ);
-  fe_mul(t, t, st.b);                           // 2^200 - 1
+  fe_sqn(t, st.b, 100); fe_mul(t, t, st.b);     // 2^200 - 1
   fe_sqn(t, t, 50);     fe_mul(t, t, st.a);     // 2^250 - 1
   fe_sqn(t, t, 2);
   fe_mul(h.X, t, st.z);        // z^((p-5)/8)

@@ -877,17 +877,19 @@ hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint3
 // prepared (pv_quad.h q_comb_side).  A block of 64 (KQ_CW + 2) threads takes 8
 // signatures: the hash wave (one lane per signature) runs the pre-checks,
 // SHA-512 and h mod L into an LDS record; the root wave (one lane per
-// signature) decodes -R -- the 250-squaring square-root chain, split around the
-// block's first barrier -- and leaves it in cached form in LDS; the KQ_CW comb
-// waves (16 lanes per signature: KQ_SIDES = 4 lane quads, two comb tables and
-// two base-point chunks each) run the comb of h and S as soon as the record is
-// there, overlapping the second half of the decode.  After the second barrier
-// side 1 adds -R and the four sides' points are summed over two exchanges
-// (shfl_xor 4, then 8): side 0 tests the total for the identity.  One wave
-// per SIMD (four waves): no two paths share an issue port.
+// signature) decodes -R -- the 250-squaring square-root chain -- and leaves it
+// in cached form in LDS; the KQ_CW comb waves (16 lanes per signature:
+// KQ_SIDES = 4 lane quads, two comb tables and two base-point chunks each) sum
+// S's base-point chunks, then run the comb of h as soon as the record is there.
+// Side 1 then adds -R and the four sides' points are summed over two exchanges
+// (shfl_xor 4, then 8): side 0 tests the total for the identity.  One wave per
+// SIMD (four waves): no two paths share an issue port.
 // Round 5: four sides instead of two -- a comb lane's chain 28 (sq + mul) +
 // 2 x 34 mul -> 28 (sq + mul) + 2 x 20 mul + one more exchange level
-// (profiles/r05_keyed_phase_kernel_stats.txt: hash -> comb was the critical path).
+// (profiles/r05_keyed_phase_kernel_stats.txt: hash -> comb was the critical path);
+// and the hand-offs are LDS flags, not block barriers: a barrier after the hash
+// held the root wave's chain until the hash was done (~7 us of a lone verify),
+// now the root chain runs uninterrupted and only the comb waves wait (kq_wait).
 // LIST: signature e of the launch is list[e] (host-buffer calls whose batch
 // mixes cached and uncached keys); else e itself, and the verdict bits also
 // go to the bitmap as the block's byte.
@@ -901,6 +903,16 @@ static_assert(KQ_CW >= 1 && 8 * KQ_LPS == 64 * KQ_CW, "comb lanes fill whole wav
 #ifndef PV_KEYED_PHASE
 #define PV_KEYED_PHASE 0
 #endif
+// a wave's LDS writes done, then the flag (lane 0); the waiting waves spin on it.
+// Every wave of the block is resident (one block = four waves on four SIMDs), so a
+// waiting wave never holds up the one it waits for.
+__device__ __forceinline__ void kq_signal(uint32_t* f) {
+  __threadfence_block();
+  if ((threadIdx.x & 63u) == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void kq_wait(uint32_t* f) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(1);
+}
 template <bool LIST>
 __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t* __restrict__ pk, int pk_by_key,
                                                                   const uint8_t* __restrict__ sig,
@@ -916,6 +928,7 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
   __shared__ uint32_t recs[8 * KQ_WORDS];
   __shared__ uint32_t negr[8 * KQ_NR];
   __shared__ uint32_t vbits[KQ_CW];
+  __shared__ uint32_t ready[2];   // 0: the records (hash wave), 1: -R (root wave)
   const int t = (int)threadIdx.x;
   const int wave = t >> 6;
   const bool comb = wave < KQ_CW;
@@ -929,8 +942,8 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
   const bool serve = !comb && k < 8 && ek < n;
   uint64_t j = 0;
   if (serve) j = LIST ? list[ek] : ek;
-  NegDecode st;
-  uint32_t enc[8];
+  if (t < 2) ready[t] = 0;
+  __syncthreads();
   if (wave == KQ_CW) {
     if (k < 8) {
       uint32_t dig[16];
@@ -941,40 +954,41 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
       }
       keyed_record(recs + KQ_WORDS * k, pre, dig);
     }
+    kq_signal(ready);
   } else if (wave == KQ_CW + 1) {
-    if (serve && !(PV_KEYED_PHASE & 1)) {
-      load8(enc, sig + 64 * j);
-      neg_decode_a(st, enc);
+    if (k < 8) {
+      uint32_t* o = negr + KQ_NR * k;
+      bool ok = false;
+      ge_p3 P;
+      if (serve && !(PV_KEYED_PHASE & 1)) {
+        uint32_t enc[8];
+        load8(enc, sig + 64 * j);
+        ok = ge_frombytes_negate(P, enc) && y_is_canonical(enc);
+      } else {
+        ge_p3_0(P);
+      }
+      ge_cached c;
+      ge_p3_to_cached(c, P);
+      fe_carry(c.YmX);
+      fe_carry(c.YpX);
+      fe_carry(c.Z2);
+      store_fe(o, c.YmX);
+      store_fe(o + 10, c.YpX);
+      store_fe(o + 20, c.T2d);
+      store_fe(o + 30, c.Z2);
+      o[40] = ok ? 1u : 0u;
     }
-  }
-  const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
-  const uint64_t ic = LIST ? list[ec] : ec;
-  qfe acc, e_hi, e_lo;
-  if (comb && !(PV_KEYED_PHASE & 2)) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
-  __syncthreads();
-  const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
-  const uint32_t* r = recs + KQ_WORDS * cs;
-  if (comb) {
+    kq_signal(ready + 1);
+  } else {
+    const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
+    const uint64_t ic = LIST ? list[ec] : ec;
+    qfe acc, e_hi, e_lo;
+    if (!(PV_KEYED_PHASE & 2)) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
+    const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
+    const uint32_t* r = recs + KQ_WORDS * cs;
+    kq_wait(ready);
     if (!(PV_KEYED_PHASE & 2)) q_comb_side(acc, r, side, kt, e_hi, e_lo, q);
-  } else if (wave == KQ_CW + 1 && k < 8) {
-    uint32_t* o = negr + KQ_NR * k;
-    bool ok = false;
-    ge_p3 P;
-    if (serve && !(PV_KEYED_PHASE & 1)) ok = neg_decode_b(P, st, enc) && y_is_canonical(enc);
-    else ge_p3_0(P);
-    ge_cached c;
-    ge_p3_to_cached(c, P);
-    fe_carry(c.YmX);
-    fe_carry(c.YpX);
-    fe_carry(c.Z2);
-    store_fe(o, c.YmX);
-    store_fe(o + 10, c.YpX);
-    store_fe(o + 20, c.T2d);
-    store_fe(o + 30, c.Z2);
-    o[40] = ok ? 1u : 0u;
-  }
-  __syncthreads();
-  if (comb) {
+    kq_wait(ready + 1);
     const uint32_t* nr = negr + KQ_NR * cs;
     qfe eR, x, xo;
     q_load_cached(eR, nr, false, q);
