@@ -118,18 +118,31 @@ struct PinBuf {
   uint8_t* p = nullptr;
   size_t cap = 0;  // bytes
   unsigned flags = hipHostMallocDefault;
+  uint8_t* dev = nullptr;  // device address of a mapped buffer (looked up once per allocation)
   hipError_t ensure(size_t n) {
     if (n <= cap && p) return hipSuccess;
     if (p) (void)hipHostFree(p);
     p = nullptr;
+    dev = nullptr;
     cap = 0;
     hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), n, flags);
+    if (e == hipSuccess && (flags & hipHostMallocMapped)) {
+      void* a = nullptr;
+      e = hipHostGetDevicePointer(&a, p, 0);
+      if (e != hipSuccess) {
+        (void)hipHostFree(p);
+        p = nullptr;
+        return e;
+      }
+      dev = static_cast<uint8_t*>(a);
+    }
     if (e == hipSuccess) cap = n;
     return e;
   }
   void release() {
     if (p) (void)hipHostFree(p);
     p = nullptr;
+    dev = nullptr;
     cap = 0;
   }
 };
@@ -420,8 +433,10 @@ struct Device {
   uint64_t lat_keyed_max = PV_LAT_KEYED_MAX;  // keyed batches up to this size: k_verify_quad_keyed
   uint64_t zc_max = PV_SMALL_ZC_MAX;          // host calls up to this size: zero-copy (tuning.small_zc_max)
   PinBuf zc_in, zc_out;                       // fine-grained page-locked image / verdicts of zero-copy calls
-  PinBuf zc_flag;                             // completion word of zero-copy calls (k_signal), polled by the host
+  PinBuf zc_flag;                             // completion word of zero-copy calls, polled by the host
   uint32_t zc_seq = 0;
+  DevBuf<uint32_t> zc_done;                   // block counter of a keyed kernel that writes the word itself
+  bool zc_done_armed = false;                 // zc_done zeroed (the kernel's last block re-arms it)
   bool lat_quad = true;              // latency kernel: k_verify_quad (lane quads); PV_LAT_PAIR: k_curve_lat
   // host-buffer chunks of generic batches: one k_chunk_half launch per chunk
   // + one k_verify_quad_list pass for the deferred records; tuning.host_fused 0:
@@ -662,6 +677,8 @@ void release_device(Device& d) {
   d.zc_in.release();
   d.zc_out.release();
   d.zc_flag.release();
+  d.zc_done.release();
+  d.zc_done_armed = false;
   d.vout.release();
   if (d.pool) d.pool->shutdown();
   d.copy = nullptr;
@@ -878,6 +895,8 @@ uint64_t small_bytes(const HostBatch& hb, uint64_t s, uint64_t e) {
 #ifndef PV_ZC_POLL
 #define PV_ZC_POLL 1
 #endif
+// all-cached zero-copy calls up to this size complete by the keyed kernel's own word
+constexpr uint64_t ZC_SELF_MAX = 128;
 // spins until *w == v (acquire) or `ns` nanoseconds have passed
 constexpr int64_t ZC_SPIN_NS = 20'000'000;
 bool spin_wait_word(const uint32_t* w, uint32_t v, int64_t ns) {
@@ -919,12 +938,8 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   const uint8_t* g = nullptr;
   uint8_t* vdst = nullptr;
   if (zc) {
-    void* a = nullptr;
-    void* b = nullptr;
-    HIP_OK(hipHostGetDevicePointer(&a, pin.p, 0));
-    HIP_OK(hipHostGetDevicePointer(&b, vout.p, 0));
-    g = static_cast<const uint8_t*>(a);
-    vdst = static_cast<uint8_t*>(b);
+    g = pin.dev;
+    vdst = vout.dev;
   } else {
     HIP_OK(d.stage.ensure(total));
     HIP_OK(d.verdict.ensure(m));
@@ -957,6 +972,18 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     }
     *reinterpret_cast<uint64_t*>(base + o_ext) = ng;
   }
+  // zero-copy calls complete by a word in fine-grained host memory that the host
+  // polls (~5 us below a stream synchronize, tools/ubench/sync_lat.hip): an
+  // all-cached call's keyed kernel writes it from its last block, other calls
+  // end with a k_signal launch
+  const bool poll = zc && PV_ZC_POLL;
+  uint32_t seq = 0;
+  bool signalled = false;
+  if (poll) {
+    HIP_OK(d.zc_flag.ensure(64));
+    if (++d.zc_seq == 0) d.zc_seq = 1;
+    seq = d.zc_seq;
+  }
   if (nk) {
     const size_t total_ext = o_ext + 8 + 8 * m;
     if (!zc) HIP_OK(hipMemcpyAsync(d.stage.p, base, total_ext, hipMemcpyHostToDevice, w.stream));
@@ -964,8 +991,19 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     if (rc) return rc;
     const uint64_t* goff = reinterpret_cast<const uint64_t*>(g);
     const uint32_t* kidx = reinterpret_cast<const uint32_t*>(g + o_ext + 8);
+    // up to 16 blocks: measured 2-3 us faster than a k_signal launch; at 125
+    // blocks 3-4 us slower (every comb wave's system-scope fence and the
+    // counter), profiles/r05_ab_completion_word.jsonl
+    const bool self = poll && ng == 0 && nk <= ZC_SELF_MAX;
+    if (self && !d.zc_done_armed) {
+      HIP_OK(d.zc_done.ensure(1));
+      HIP_OK(hipMemsetAsync(d.zc_done.p, 0, sizeof(uint32_t), w.stream));
+      d.zc_done_armed = true;
+    }
     HIP_OK(pv::launch_verify_quad_keyed(g + o_pk, false, g + o_sig, g + o_blob, goff, nk, kidx + m, d.kc.p, kidx,
-                                        d.bw.p, vdst, nullptr, w.stream));
+                                        d.bw.p, vdst, nullptr, w.stream, self ? d.zc_done.p : nullptr,
+                                        self ? reinterpret_cast<uint32_t*>(d.zc_flag.dev) : nullptr, seq));
+    signalled = self;
     if (ng)
       HIP_OK(pv::launch_verify_quad_list(g + o_pk, g + o_sig, g + o_blob, goff, kidx + 2 * m - ng,
                                          reinterpret_cast<const unsigned long long*>(g + o_ext), ng, (int)((ng + 7) / 8),
@@ -978,17 +1016,10 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
                                   vdst, nullptr, w.stream, false, nullptr, nullptr);
     if (rc) return rc;
   }
-  if (zc && PV_ZC_POLL) {
-    // completion by polling a word k_signal writes after the verify kernels:
-    // ~5 us below a stream synchronize per call (profiles/r05_keyed4_phase_and_sync.jsonl,
-    // tools/ubench/sync_lat.hip); past the spin budget (a fault, a long queue)
-    // the synchronize reports / waits as before
-    HIP_OK(d.zc_flag.ensure(64));
-    void* fp = nullptr;
-    HIP_OK(hipHostGetDevicePointer(&fp, d.zc_flag.p, 0));
-    if (++d.zc_seq == 0) d.zc_seq = 1;
-    const uint32_t seq = d.zc_seq;
-    HIP_OK(pv::launch_signal(static_cast<uint32_t*>(fp), seq, w.stream));
+  if (poll) {
+    // past the spin budget (a fault, a long queue) the synchronize reports /
+    // waits as before
+    if (!signalled) HIP_OK(pv::launch_signal(reinterpret_cast<uint32_t*>(d.zc_flag.dev), seq, w.stream));
     drain.done = spin_wait_word(reinterpret_cast<const uint32_t*>(d.zc_flag.p), seq, ZC_SPIN_NS);
     if (!drain.done) HIP_OK(hipStreamSynchronize(w.stream));
   } else {

@@ -120,11 +120,14 @@ hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint3
 // signatures in one launch, signature e's key = ktab entry kidx[i] with i =
 // list ? list[e] : e; the hashed key bytes are pk + 32 * (pk_by_key ? kidx[i] : i).
 // Verdicts go to verdict[i]; bitmap (ceil(n/64) words, needs no zeroing) only
-// without a list (may be NULL then too)
+// without a list (may be NULL then too).  flag (host-mapped) / done (a device
+// counter at 0): the last block writes seq to *flag when every verdict is out
+// and re-arms *done (both NULL: no completion word)
 hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uint8_t* sig, const uint8_t* blob,
                                     const uint64_t* off, uint64_t n, const uint32_t* list, const uint32_t* ktab,
                                     const uint32_t* kidx, const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap,
-                                    hipStream_t s);
+                                    hipStream_t s, uint32_t* done = nullptr, uint32_t* flag = nullptr,
+                                    uint32_t seq = 0);
 
 // completion signal of a zero-copy host call: *flag = seq (system scope, after
 // every earlier kernel of the stream), polled by the host instead of a stream

@@ -924,7 +924,8 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
                                                                   const uint32_t* __restrict__ bw,
                                                                   uint8_t* __restrict__ verdict,
                                                                   uint8_t* __restrict__ bitmap_bytes,
-                                                                  uint64_t bitmap_len) {
+                                                                  uint64_t bitmap_len, uint32_t* __restrict__ done,
+                                                                  uint32_t* __restrict__ flag, uint32_t seq) {
   __shared__ uint32_t recs[8 * KQ_WORDS];
   __shared__ uint32_t negr[8 * KQ_NR];
   __shared__ uint32_t vbits[KQ_CW];
@@ -1008,6 +1009,7 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && nr[40] != 0 && id;
     const bool mine = side == 0 && (t & 3) == 0 && e < n;
     if (mine) verdict[ic] = v ? 1 : 0;
+    if (flag) __threadfence_system();   // the verdicts out before the completion word
     if constexpr (!LIST) {
       const uint64_t ball = __ballot(mine && v);   // bit KQ_LPS m: signature 64 wave / KQ_LPS + m
       if ((t & 63) == 0) {
@@ -1029,12 +1031,27 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
         for (uint64_t b = (uint64_t)blockIdx.x + 1; b < bitmap_len; ++b) bitmap_bytes[b] = 0;
     }
   }
+  if (flag) {
+    // completion word of a zero-copy host call (run_small): the last block to
+    // finish writes seq into fine-grained host memory and re-arms the counter
+    // (instead of a k_signal launch behind the kernel)
+    if constexpr (LIST) __syncthreads();
+    if (t == 0) {
+      __threadfence_system();
+      if (atomicAdd(done, 1u) + 1u == gridDim.x) {
+        done[0] = 0;
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
 }
 
 hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uint8_t* sig, const uint8_t* blob,
                                     const uint64_t* off, uint64_t n, const uint32_t* list, const uint32_t* ktab,
                                     const uint32_t* kidx, const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap,
-                                    hipStream_t s) {
+                                    hipStream_t s, uint32_t* done, uint32_t* flag, uint32_t seq) {
+  if ((flag != nullptr) != (done != nullptr)) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + 7) / 8;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
@@ -1042,11 +1059,12 @@ hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uin
   const uint64_t bytes = (n + 63) / 64 * 8;
   if (list)
     hipLaunchKernelGGL(k_verify_quad_keyed<true>, dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
-                       pk_by_key ? 1 : 0, sig, blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0);
+                       pk_by_key ? 1 : 0, sig, blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0, done, flag,
+                       seq);
   else
     hipLaunchKernelGGL(k_verify_quad_keyed<false>, dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
                        pk_by_key ? 1 : 0, sig, blob, off, n, nullptr, ktab, kidx, bw, verdict,
-                       reinterpret_cast<uint8_t*>(bitmap), bytes);
+                       reinterpret_cast<uint8_t*>(bitmap), bytes, done, flag, seq);
   return hipGetLastError();
 }
 

@@ -377,7 +377,15 @@ def shutdown():
 
 
 def _ptr(a):
-    return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else ctypes.c_void_p(0)
+    """address of a contiguous array's data, for a c_void_p argument (None if empty).
+    The buffer-protocol form costs ~0.8 us against ~2 us for `a.ctypes.data`, which
+    matters at five pointers per latency call; read-only arrays take the slow path."""
+    if a is None or not a.size:
+        return None
+    try:
+        return ctypes.addressof(ctypes.c_char.from_buffer(a))
+    except (TypeError, ValueError, BufferError):
+        return a.ctypes.data
 
 
 try:  # native host preprocessing (csrc/pv_host.cpp); the Python packer covers its Fallback cases

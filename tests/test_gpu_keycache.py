@@ -151,3 +151,27 @@ def test_wide_keys_c3_shape_and_adversarial(nat, adversarial):
     got = verdict.cpu().numpy().astype(bool)
     wrong = [rows[k][0] for k in range(len(rows)) if got[k] != rows[k][3]]
     assert not wrong, wrong
+
+
+def test_completion_word_over_many_calls(nat, raw_vectors):
+    """Zero-copy calls complete by a word the host polls: all-cached calls get it
+    from the keyed kernel's last block (a device block counter it re-arms), mixed
+    and uncached calls from k_signal.  Interleave the three kinds over 120 calls of
+    ragged sizes (1..1,000 signatures, 1..125 blocks) so that every sequence
+    number, counter re-arm and hand-over between the two completion paths is
+    exercised; each call must return its own fixture verdicts."""
+    r = raw_vectors
+    want = r['verdict'].astype(bool)
+    nat.keycache_add(r['pk'][:1500])
+    rng = np.random.default_rng(7)
+    for c in range(120):
+        n = int(rng.choice([1, 2, 7, 8, 9, 63, 64, 65, 250, 1000]))
+        kind = c % 3
+        if kind == 0:     # every key cached: the kernel writes the word
+            start = int(rng.integers(0, 1500 - n + 1))
+        elif kind == 1:   # straddles the cached range: keyed + list kernels, then k_signal
+            start = max(0, 1500 - n // 2 - 1)
+        else:             # no key cached: the generic latency kernel, then k_signal
+            start = int(rng.integers(1500, len(want) - n + 1))
+        got = nat.verify_batch_arrays(*_slice(r, start, n))
+        assert (got == want[start:start + n]).all(), (c, kind, start, n)
