@@ -898,6 +898,7 @@ constexpr int KQ_LPS = 4 * KQ_SIDES;   // lanes per signature in the comb waves
 constexpr int KQ_CW = 8 * KQ_LPS / 64;   // comb waves per block (8 signatures)
 constexpr int KQ_THREADS = 64 * (KQ_CW + 2);
 static_assert(KQ_CW >= 1 && 8 * KQ_LPS == 64 * KQ_CW, "comb lanes fill whole waves");
+static_assert(KQ_SCHED_BLOCKS >= 1 && KQ_SCHED_BLOCKS <= 8, "one lane per (signature, block) of the hash wave");
 // PV_KEYED_PHASE (timing variants only, wrong verdicts), a bit mask: 1 skips the
 // -R square root (root wave), 2 the comb (comb waves), 4 the hash (hash wave)
 #ifndef PV_KEYED_PHASE
@@ -930,6 +931,9 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
   __shared__ uint32_t negr[8 * KQ_NR];
   __shared__ uint32_t vbits[KQ_CW];
   __shared__ uint32_t ready[2];   // 0: the records (hash wave), 1: -R (root wave)
+  // the hash wave's message schedules: block b < KQ_SCHED_BLOCKS of signature s at
+  // lane 8 b + s, K_t + W_t at kws[t * 8 KQ_SCHED_BLOCKS + lane]
+  __shared__ uint64_t kws[80 * 8 * KQ_SCHED_BLOCKS];
   const int t = (int)threadIdx.x;
   const int wave = t >> 6;
   const bool comb = wave < KQ_CW;
@@ -946,13 +950,27 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
   if (t < 2) ready[t] = 0;
   __syncthreads();
   if (wave == KQ_CW) {
+    // SHA-512(R || A || M) with the message schedules of the first
+    // KQ_SCHED_BLOCKS blocks computed by one lane per block first (all blocks'
+    // loads in flight at once), then the hashing lane runs only the rounds of
+    // those blocks (round 5: the hash -> comb path is the kernel's critical path)
+    const int sb = k & 7, bb = k >> 3;   // this lane's signature and block
+    const uint64_t es = e0 + (uint64_t)sb;
+    const bool serve_s = !(PV_KEYED_PHASE & 4) && bb < KQ_SCHED_BLOCKS && es < n;
+    uint64_t js = 0;
+    if (serve_s) js = LIST ? list[es] : es;
+    const uint8_t* as = pk + 32 * (pk_by_key ? (uint64_t)kidx[js] : js);
+    const uint64_t mlen_s = serve_s ? off[js + 1] - off[js] : 0;
+    const uint64_t nb_s = hram_blocks(mlen_s);
+    if (serve_s && (uint64_t)bb < nb_s)
+      keyed_sched_block(kws + k, 8 * KQ_SCHED_BLOCKS, sig + 64 * js, as, blob + off[js], mlen_s, (uint64_t)bb);
+    __threadfence_block();   // the schedules in LDS before the hashing lanes read them (same wave)
+    __builtin_amdgcn_wave_barrier();
     if (k < 8) {
       uint32_t dig[16];
       bool pre = false;
-      if (serve && !(PV_KEYED_PHASE & 4)) {
-        const uint8_t* a = pk + 32 * (pk_by_key ? (uint64_t)kidx[j] : j);
-        pre = hash_one(dig, a, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
-      }
+      if (serve && !(PV_KEYED_PHASE & 4))
+        pre = keyed_hash(dig, kws + k, 8 * KQ_SCHED_BLOCKS, 8, sig + 64 * j, as, blob + off[j], mlen_s);
       keyed_record(recs + KQ_WORDS * k, pre, dig);
     }
     kq_signal(ready);

@@ -438,6 +438,38 @@ PV_HD void keyed_record(uint32_t* rec, bool pre, const uint32_t dig[16]) {
   rec[KQ_OK] = pre ? 1u : 0u;
 }
 
+// SHA-512(R || A || M) as k_verify_quad_keyed's hash wave forms it (round 5):
+// the message schedules of the first KQ_SCHED_BLOCKS blocks are computed first,
+// one lane per (signature, block) of the wave (keyed_sched_block, all blocks'
+// loads in flight at once), and the hashing lane runs only their 80 rounds
+// (keyed_hash); later blocks are scheduled inline as in hash_one.  The same
+// words as hash_one: the schedule is sha512_compress's, split in two.
+constexpr int KQ_SCHED_BLOCKS = 4;   // messages up to 431 bytes
+PV_HD void keyed_sched_block(uint64_t* kw, int stride, const uint8_t* sig, const uint8_t* pk, const uint8_t* m,
+                             uint64_t mlen, uint64_t b) {
+  uint64_t w[16];
+  hram_block(w, sig, pk, m, mlen, b, hram_blocks(mlen));
+  sha512_schedule_kw(kw, stride, w);
+}
+// kw + b * bstride: block b's K_t + W_t at stride `stride` (b < KQ_SCHED_BLOCKS)
+PV_HD bool keyed_hash(uint32_t dig[16], const uint64_t* kw, int stride, int bstride, const uint8_t* sig,
+                      const uint8_t* pk, const uint8_t* m, uint64_t mlen) {
+  if (!precheck(pk, sig)) return false;
+  uint64_t h[8], w[16];
+  sha512_init(h);
+  const uint64_t nb = hram_blocks(mlen);
+  for (uint64_t b = 0; b < nb; ++b) {
+    if (b < (uint64_t)KQ_SCHED_BLOCKS) {
+      sha512_compress_kw(h, kw + b * (uint64_t)bstride, stride);
+    } else {
+      hram_block(w, sig, pk, m, mlen, b, nb);
+      sha512_compress(h, w);
+    }
+  }
+  sha512_digest_words(dig, h);
+  return true;
+}
+
 // S's share of the comb, which needs no hash: with the signed radix-2^16
 // digits of S (offset form), side s sums its chunks q = KQ_TPS s .. of the
 // high halves (added at window 4, i.e. doubled 16 times) and of the low halves

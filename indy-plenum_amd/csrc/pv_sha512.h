@@ -166,6 +166,40 @@ PV_HD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
 }
 
+// The compression split in two (k_verify_quad_keyed's hash wave: one lane per
+// message block computes that block's schedule, the hashing lane then runs
+// only the 80 rounds).  kw[t * stride] = K_t + W_t for t < 80 from the block's
+// 16 big-endian words; the same sums as sha512_compress's rolling schedule.
+PV_HD void sha512_schedule_kw(uint64_t* kw, int stride, const uint64_t w0[16]) {
+  uint64_t w[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    w[j] = w0[j];
+    kw[j * stride] = PV_SHA512_K[j] + w[j];
+  }
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
+#pragma clang loop unroll(full)
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), shr64(w15, 7));
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), shr64(w2, 6));
+      w[j] = add64(add64(add64(w[j], w[(j + 9) & 15]), s0), s1);
+      kw[(r + j) * stride] = PV_SHA512_K[r + j] + w[j];
+    }
+  }
+}
+PV_HD void sha512_compress_kw(uint64_t h[8], const uint64_t* kw, int stride) {
+  PV_COUNT(sha);
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
+#pragma clang loop unroll(full)
+    for (int j = 0; j < 16; ++j) sha512_round(a, b, c, d, e, f, g, k, kw[(r + j) * stride]);
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+}
+
 PV_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }

@@ -319,7 +319,12 @@ void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
   const QRole qr = qrole_of(0);
   for (uint64_t i = 0; i < n; ++i) {
     uint32_t dig[16], rec[KQ_WORDS];
-    const bool pre = hash_one(dig, pk + 32 * kidx[i], sig + 64 * i, blob + off[i], off[i + 1] - off[i]);
+    // the hash wave's split: schedules of the first KQ_SCHED_BLOCKS blocks, then the rounds
+    const uint64_t mlen = off[i + 1] - off[i];
+    uint64_t kw[80 * KQ_SCHED_BLOCKS];
+    for (uint64_t b = 0; b < (uint64_t)KQ_SCHED_BLOCKS && b < hram_blocks(mlen); ++b)
+      keyed_sched_block(kw + b, KQ_SCHED_BLOCKS, sig + 64 * i, pk + 32 * kidx[i], blob + off[i], mlen, b);
+    const bool pre = keyed_hash(dig, kw, KQ_SCHED_BLOCKS, 1, sig + 64 * i, pk + 32 * kidx[i], blob + off[i], mlen);
     keyed_record(rec, pre, dig);
     uint32_t nr[41];
     keyed_neg_r(nr, sig + 64 * i);
