@@ -339,7 +339,45 @@ PyObject* pack_items(PyObject* snap) {
   return r;
 }
 
+// verify_batch(fn, pk, sig, blob, off, verdict, device_mask, flags) -> rc:
+// pv_verify_batch (include/plenum_verify.h; `fn` = its address, from the ctypes
+// binding) called on the buffers of C-contiguous arrays, the GIL released.  The
+// ctypes call converts five pointers at ~0.6 us each; a lone cached verify is
+// ~80 us, so the plenum_gpu wrapper takes this path when the module is built.
+using verify_fn = int (*)(const uint8_t*, const uint8_t*, const uint8_t*, const uint64_t*, uint64_t, uint8_t*,
+                          uint32_t, uint32_t);
+PyObject* verify_batch(PyObject*, PyObject* args) {
+  unsigned long long fn = 0;
+  PyObject *o[5];
+  unsigned int mask = 0, flags = 0;
+  if (!PyArg_ParseTuple(args, "KOOOOOII", &fn, &o[0], &o[1], &o[2], &o[3], &o[4], &mask, &flags)) return nullptr;
+  if (!fn) return fallback();
+  Py_buffer b[5];
+  int got = 0;
+  for (; got < 5; ++got) {
+    const int req = got == 4 ? (PyBUF_SIMPLE | PyBUF_WRITABLE) : PyBUF_SIMPLE;
+    if (PyObject_GetBuffer(o[got], &b[got], req) != 0) break;
+  }
+  if (got < 5) {
+    for (int i = 0; i < got; ++i) PyBuffer_Release(&b[i]);
+    PyErr_Clear();
+    return fallback();
+  }
+  const uint64_t n = (uint64_t)b[4].len;   // one verdict byte per signature
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = reinterpret_cast<verify_fn>((uintptr_t)fn)(static_cast<const uint8_t*>(b[0].buf),
+                                                  static_cast<const uint8_t*>(b[1].buf),
+                                                  static_cast<const uint8_t*>(b[2].buf),
+                                                  static_cast<const uint64_t*>(b[3].buf), n,
+                                                  static_cast<uint8_t*>(b[4].buf), mask, flags);
+  Py_END_ALLOW_THREADS
+  for (int i = 0; i < 5; ++i) PyBuffer_Release(&b[i]);
+  return PyLong_FromLong(rc);
+}
+
 PyMethodDef kMethods[] = {
+    {"verify_batch", verify_batch, METH_VARARGS, "pv_verify_batch(fn address, pk, sig, blob, off, verdict, mask, flags) -> rc"},
     {"pack", pack, METH_O, "pack a list of bytes-like messages -> (blob, u64 offsets)"},
     {"b58decode", b58decode, METH_O, "base58 decode (str or bytes) -> bytes"},
     {"b58encode", b58encode, METH_O, "base58 encode (bytes or str) -> bytes"},

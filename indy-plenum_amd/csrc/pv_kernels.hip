@@ -875,7 +875,8 @@ hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint3
 
 // k_verify_quad_keyed: the latency verdict of signatures whose key is
 // prepared (pv_quad.h q_comb_side).  A block of 64 (KQ_CW + 2) threads takes 8
-// signatures: the hash wave (one lane per signature) runs the pre-checks,
+// signatures (4 in the small-call form, with 8 comb sides each: SIG below):
+// the hash wave (one lane per signature) runs the pre-checks,
 // SHA-512 and h mod L into an LDS record; the root wave (one lane per
 // signature) decodes -R -- the 250-squaring square-root chain -- and leaves it
 // in cached form in LDS; the KQ_CW comb waves (16 lanes per signature:
@@ -894,11 +895,9 @@ hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint3
 // mixes cached and uncached keys); else e itself, and the verdict bits also
 // go to the bitmap as the block's byte.
 constexpr int KQ_NR = 41;   // -R cached in add order (Y-X, Y+X, 2dT, 2Z) + decode verdict
-constexpr int KQ_LPS = 4 * KQ_SIDES;   // lanes per signature in the comb waves
-constexpr int KQ_CW = 8 * KQ_LPS / 64;   // comb waves per block (8 signatures)
+constexpr int KQ_CW = 2;   // comb waves per block: 8 signatures x 4 sides, or 4 x 8 (small calls)
 constexpr int KQ_THREADS = 64 * (KQ_CW + 2);
-static_assert(KQ_CW >= 1 && 8 * KQ_LPS == 64 * KQ_CW, "comb lanes fill whole waves");
-static_assert(KQ_SCHED_BLOCKS >= 1 && KQ_SCHED_BLOCKS <= 8, "one lane per (signature, block) of the hash wave");
+static_assert(KQ_SCHED_BLOCKS >= 1 && 8 * KQ_SCHED_BLOCKS <= 64, "one lane per (signature, block) of the hash wave");
 // PV_KEYED_PHASE (timing variants only, wrong verdicts), a bit mask: 1 skips the
 // -R square root (root wave), 2 the comb (comb waves), 4 the hash (hash wave)
 #ifndef PV_KEYED_PHASE
@@ -914,7 +913,10 @@ __device__ __forceinline__ void kq_signal(uint32_t* f) {
 __device__ __forceinline__ void kq_wait(uint32_t* f) {
   while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(1);
 }
-template <bool LIST>
+// SIG signatures per block: 8 (SIDES = 4 lane quads each) or, for small host
+// calls, 4 (SIDES = 8: a comb lane adds one key table and one base-point chunk);
+// the bitmap form (no LIST) needs 8 (one bitmap byte per block)
+template <bool LIST, int SIG>
 __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t* __restrict__ pk, int pk_by_key,
                                                                   const uint8_t* __restrict__ sig,
                                                                   const uint8_t* __restrict__ blob,
@@ -927,24 +929,28 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
                                                                   uint8_t* __restrict__ bitmap_bytes,
                                                                   uint64_t bitmap_len, uint32_t* __restrict__ done,
                                                                   uint32_t* __restrict__ flag, uint32_t seq) {
-  __shared__ uint32_t recs[8 * KQ_WORDS];
-  __shared__ uint32_t negr[8 * KQ_NR];
+  constexpr int SIDES = 32 / SIG;      // lane quads per signature
+  constexpr int LPS = 4 * SIDES;       // comb lanes per signature
+  constexpr int KSL = SIG * KQ_SCHED_BLOCKS;   // schedule lanes of the hash wave
+  static_assert((SIG == 8 || (SIG == 4 && LIST)) && SIG * LPS == 64 * KQ_CW, "8, or 4 with a list");
+  __shared__ uint32_t recs[SIG * KQ_WORDS];
+  __shared__ uint32_t negr[SIG * KQ_NR];
   __shared__ uint32_t vbits[KQ_CW];
   __shared__ uint32_t ready[2];   // 0: the records (hash wave), 1: -R (root wave)
   // the hash wave's message schedules: block b < KQ_SCHED_BLOCKS of signature s at
-  // lane 8 b + s, K_t + W_t at kws[t * 8 KQ_SCHED_BLOCKS + lane]
-  __shared__ uint64_t kws[80 * 8 * KQ_SCHED_BLOCKS];
+  // lane SIG b + s, K_t + W_t at kws[t * KSL + lane]
+  __shared__ uint64_t kws[80 * KSL];
   const int t = (int)threadIdx.x;
   const int wave = t >> 6;
   const bool comb = wave < KQ_CW;
-  const uint64_t e0 = (uint64_t)blockIdx.x * 8;
-  const int side = (t >> 2) & (KQ_SIDES - 1);
+  const uint64_t e0 = (uint64_t)blockIdx.x * SIG;
+  const int side = (t >> 2) & (SIDES - 1);
   const QRole q = qrole_of((uint32_t)t & 3u);
-  const int cs = comb ? t / KQ_LPS : 0;   // comb waves: the block's signature of this lane
+  const int cs = comb ? t / LPS : 0;   // comb waves: the block's signature of this lane
   const uint64_t e = e0 + (uint64_t)cs;
-  const int k = (t & 63);                 // hash / root wave: lane k < 8 serves signature e0 + k
+  const int k = (t & 63);                 // hash / root wave: lane k < SIG serves signature e0 + k
   const uint64_t ek = e0 + (uint64_t)k;
-  const bool serve = !comb && k < 8 && ek < n;
+  const bool serve = !comb && k < SIG && ek < n;
   uint64_t j = 0;
   if (serve) j = LIST ? list[ek] : ek;
   if (t < 2) ready[t] = 0;
@@ -954,7 +960,7 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     // KQ_SCHED_BLOCKS blocks computed by one lane per block first (all blocks'
     // loads in flight at once), then the hashing lane runs only the rounds of
     // those blocks (round 5: the hash -> comb path is the kernel's critical path)
-    const int sb = k & 7, bb = k >> 3;   // this lane's signature and block
+    const int sb = k % SIG, bb = k / SIG;   // this lane's signature and block
     const uint64_t es = e0 + (uint64_t)sb;
     const bool serve_s = !(PV_KEYED_PHASE & 4) && bb < KQ_SCHED_BLOCKS && es < n;
     uint64_t js = 0;
@@ -963,19 +969,19 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     const uint64_t mlen_s = serve_s ? off[js + 1] - off[js] : 0;
     const uint64_t nb_s = hram_blocks(mlen_s);
     if (serve_s && (uint64_t)bb < nb_s)
-      keyed_sched_block(kws + k, 8 * KQ_SCHED_BLOCKS, sig + 64 * js, as, blob + off[js], mlen_s, (uint64_t)bb);
+      keyed_sched_block(kws + k, KSL, sig + 64 * js, as, blob + off[js], mlen_s, (uint64_t)bb);
     __threadfence_block();   // the schedules in LDS before the hashing lanes read them (same wave)
     __builtin_amdgcn_wave_barrier();
-    if (k < 8) {
+    if (k < SIG) {
       uint32_t dig[16];
       bool pre = false;
       if (serve && !(PV_KEYED_PHASE & 4))
-        pre = keyed_hash(dig, kws + k, 8 * KQ_SCHED_BLOCKS, 8, sig + 64 * j, as, blob + off[j], mlen_s);
+        pre = keyed_hash(dig, kws + k, KSL, SIG, sig + 64 * j, as, blob + off[j], mlen_s);
       keyed_record(recs + KQ_WORDS * k, pre, dig);
     }
     kq_signal(ready);
   } else if (wave == KQ_CW + 1) {
-    if (k < 8) {
+    if (k < SIG) {
       uint32_t* o = negr + KQ_NR * k;
       bool ok = false;
       ge_p3 P;
@@ -1002,11 +1008,11 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     const uint64_t ec = e < n ? e : n - 1;   // lanes past the batch run on the last signature (results dropped)
     const uint64_t ic = LIST ? list[ec] : ec;
     qfe acc, e_hi, e_lo;
-    if (!(PV_KEYED_PHASE & 2)) q_comb_base(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
+    if (!(PV_KEYED_PHASE & 2)) q_comb_base<SIDES>(e_hi, e_lo, sig + 64 * ic, side, bw, q);   // S B: no hash needed
     const uint32_t* kt = ktab + (uint64_t)kidx[ic] * KEY_WORDS;
     const uint32_t* r = recs + KQ_WORDS * cs;
     kq_wait(ready);
-    if (!(PV_KEYED_PHASE & 2)) q_comb_side(acc, r, side, kt, e_hi, e_lo, q);
+    if (!(PV_KEYED_PHASE & 2)) q_comb_side<SIDES>(acc, r, side, kt, e_hi, e_lo, q);
     kq_wait(ready + 1);
     const uint32_t* nr = negr + KQ_NR * cs;
     qfe eR, x, xo;
@@ -1014,7 +1020,7 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     q_keyed_add_negr(acc, eR, side, q);
     // the sides' sum: side s + 1 -> s for even s (xor 4), then side 2 -> 0 (xor 8) ...
 #pragma unroll
-    for (int step = 1; step < KQ_SIDES / 2; step <<= 1) {
+    for (int step = 1; step < SIDES / 2; step <<= 1) {
       q_to_cached(x, acc, q);
 #pragma unroll
       for (int i = 0; i < 10; ++i) xo.l[0].v[i] = __shfl_xor(x.l[0].v[i], 4 * step, 64);
@@ -1022,18 +1028,18 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     }
     q_to_cached(x, acc, q);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) xo.l[0].v[i] = __shfl_xor(x.l[0].v[i], 2 * KQ_SIDES, 64);   // side S/2 -> 0
+    for (int i = 0; i < 10; ++i) xo.l[0].v[i] = __shfl_xor(x.l[0].v[i], 2 * SIDES, 64);   // side S/2 -> 0
     const bool id = q_sum_is_identity(acc, xo, q);
     const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && nr[40] != 0 && id;
     const bool mine = side == 0 && (t & 3) == 0 && e < n;
     if (mine) verdict[ic] = v ? 1 : 0;
     if (flag) __threadfence_system();   // the verdicts out before the completion word
     if constexpr (!LIST) {
-      const uint64_t ball = __ballot(mine && v);   // bit KQ_LPS m: signature 64 wave / KQ_LPS + m
+      const uint64_t ball = __ballot(mine && v);   // bit LPS m: signature 64 wave / LPS + m
       if ((t & 63) == 0) {
         uint32_t bits = 0;
 #pragma unroll
-        for (int m = 0; m < 64 / KQ_LPS; ++m) bits |= (uint32_t)((ball >> (KQ_LPS * m)) & 1ull) << m;
+        for (int m = 0; m < 64 / LPS; ++m) bits |= (uint32_t)((ball >> (LPS * m)) & 1ull) << m;
         vbits[wave] = bits;
       }
     }
@@ -1043,7 +1049,7 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     if (t == 0 && bitmap_bytes) {
       uint32_t bits = 0;
 #pragma unroll
-      for (int w = 0; w < KQ_CW; ++w) bits |= vbits[w] << (w * (64 / KQ_LPS));
+      for (int w = 0; w < KQ_CW; ++w) bits |= vbits[w] << (w * (64 / LPS));
       bitmap_bytes[blockIdx.x] = (uint8_t)bits;
       if ((uint64_t)blockIdx.x + 1 == gridDim.x)
         for (uint64_t b = (uint64_t)blockIdx.x + 1; b < bitmap_len; ++b) bitmap_bytes[b] = 0;
@@ -1065,6 +1071,10 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
   }
 }
 
+// host-buffer (list) calls up to this size take the 4-signature blocks
+#ifndef KQ_SMALL_MAX
+#define KQ_SMALL_MAX 1024
+#endif
 hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uint8_t* sig, const uint8_t* blob,
                                     const uint64_t* off, uint64_t n, const uint32_t* list, const uint32_t* ktab,
                                     const uint32_t* kidx, const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap,
@@ -1075,12 +1085,16 @@ hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uin
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
   if (list && bitmap) return hipErrorInvalidValue;
   const uint64_t bytes = (n + 63) / 64 * 8;
-  if (list)
-    hipLaunchKernelGGL(k_verify_quad_keyed<true>, dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
+  if (list && n <= KQ_SMALL_MAX)   // small host calls: 4 signatures per block, 8 comb sides each
+    hipLaunchKernelGGL((k_verify_quad_keyed<true, 4>), dim3((uint32_t)((n + 3) / 4)), dim3(KQ_THREADS), 0, s, pk,
+                       pk_by_key ? 1 : 0, sig, blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0, done, flag,
+                       seq);
+  else if (list)
+    hipLaunchKernelGGL((k_verify_quad_keyed<true, 8>), dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
                        pk_by_key ? 1 : 0, sig, blob, off, n, list, ktab, kidx, bw, verdict, nullptr, 0, done, flag,
                        seq);
   else
-    hipLaunchKernelGGL(k_verify_quad_keyed<false>, dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
+    hipLaunchKernelGGL((k_verify_quad_keyed<false, 8>), dim3((uint32_t)blocks), dim3(KQ_THREADS), 0, s, pk,
                        pk_by_key ? 1 : 0, sig, blob, off, n, nullptr, ktab, kidx, bw, verdict,
                        reinterpret_cast<uint8_t*>(bitmap), bytes, done, flag, seq);
   return hipGetLastError();

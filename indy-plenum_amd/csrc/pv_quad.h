@@ -412,17 +412,18 @@ PV_HD bool q_sum_is_identity(const qfe& Q0, const qfe& e1, const QRole& q) {
 // (double_scalarmult_comb's schedule), split over the signature's KQ_SIDES
 // lane quads: side s adds the key tables and the base-point chunks
 // q = (8 / KQ_SIDES) s ..  + 8 / KQ_SIDES - 1, so with four sides a lane runs
-// 28 (sq + mul) + 20 x 2 mul (two sides: 28 (sq + mul) + 40 x 2 mul).  The
-// sides' points are then summed over a tree of exchanges (the kernel's
-// shfl_xor 4 and 8; hc_verify_keyed_quad on the host).  libsodium accepts iff
+// 28 (sq + mul) + 20 x 2 mul (two sides: 28 (sq + mul) + 40 x 2 mul; eight,
+// the small-call form: 28 (sq + mul) + 10 x 2 mul).  The sides' points are
+// then summed over a tree of exchanges (the kernel's shfl_xor 4, 8, 16;
+// hc_verify_keyed_quad on the host).  libsodium accepts iff
 // encode(R') == R, i.e. iff R decodes with a canonical y and R' + (-R) = O (the
 // identity test of the half-size path, pv_lattice.h): -R is decoded while the
 // scalar wave hashes, side 1 adds it, and side 0 tests the total for O.
 //
 // record (LDS): h + the radix-16 digit offsets (8 words), pre-check verdict
 constexpr int KQ_H = 0, KQ_OK = 8, KQ_WORDS = 9;
-constexpr int KQ_SIDES = 4;   // lane quads per signature in k_verify_quad_keyed
-constexpr int KQ_TPS = 8 / KQ_SIDES;   // comb tables (and base-point chunks) per side
+constexpr int KQ_SIDES = 4;   // lane quads per signature in k_verify_quad_keyed (8 per block)
+constexpr int KQ_SIDES_SMALL = 8;   // ... in its small-call form (4 signatures per block)
 
 PV_HD void keyed_record(uint32_t* rec, bool pre, const uint32_t dig[16]) {
   uint32_t hh[8];
@@ -471,11 +472,13 @@ PV_HD bool keyed_hash(uint32_t dig[16], const uint64_t* kw, int stride, int bstr
 }
 
 // S's share of the comb, which needs no hash: with the signed radix-2^16
-// digits of S (offset form), side s sums its chunks q = KQ_TPS s .. of the
+// digits of S (offset form), side s sums its chunks q = (8 / SIDES) s .. of the
 // high halves (added at window 4, i.e. doubled 16 times) and of the low halves
 // (added last) into two points, returned in cached add order.  Runs while the
 // scalar wave hashes.
+template <int SIDES = KQ_SIDES>
 PV_HD void q_comb_base(qfe& e_hi, qfe& e_lo, const uint8_t* sig, int side, const uint32_t* bw, const QRole& q) {
+  constexpr int KQ_TPS = 8 / SIDES;   // comb tables (and base-point chunks) per side
   uint32_t sp[8];
   load8(sp, sig + 32);
   sc_add_pattern(sp, sp, HALF_S_PATTERN);
@@ -504,12 +507,14 @@ PV_HD void q_comb_base(qfe& e_hi, qfe& e_lo, const uint8_t* sig, int side, const
   q_to_cached(e_lo, pl, q);
 }
 
-// h's share of the comb on side s: the key tables q = KQ_TPS s .. (kt = the
+// h's share of the comb on side s: the key tables q = (8 / SIDES) s .. (kt = the
 // key's 8 comb tables), 8 windows of 4 doublings; the base-point sums of
 // q_comb_base join at window 4 (e_hi) and after the last window (e_lo).  Each
 // window's key entries are fetched before its doublings.
+template <int SIDES = KQ_SIDES>
 PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* kt, const qfe& e_hi, const qfe& e_lo,
                        const QRole& q) {
+  constexpr int KQ_TPS = 8 / SIDES;
   uint32_t hp[KQ_TPS];
 #pragma unroll
   for (int k = 0; k < KQ_TPS; ++k) hp[k] = rec[KQ_H + KQ_TPS * side + k];

@@ -428,7 +428,8 @@ def test_keyed_wide_raw_vectors_and_op_counts(hc, raw_vectors):
     assert abs(prep_mul - bench.W_MUL_KEYPREP_WIDE) <= 128, prep_mul
 
 
-def _run_keyed_quad(hc, pk, sig, blob, off):
+def _run_keyed_quad(hc, pk, sig, blob, off, small=False):
+    """small: the 4-signature-block form (8 comb sides per signature)"""
     upk, kidx = np.unique(pk, axis=0, return_inverse=True)
     kidx = np.ascontiguousarray(kidx.reshape(-1), np.uint32)
     upk = np.ascontiguousarray(upk, np.uint8)
@@ -436,30 +437,35 @@ def _run_keyed_quad(hc, pk, sig, blob, off):
     v = np.zeros(n, np.uint8)
     b = orc.padded(blob)
     hc.hc_reset_counts()
-    hc.hc_verify_keyed_quad(_p(upk), ctypes.c_uint64(len(upk)), _p(kidx), _p(np.ascontiguousarray(sig)), _p(b),
-                            _p(np.ascontiguousarray(off)), ctypes.c_uint64(n), _p(v))
+    fn = hc.hc_verify_keyed_quad_small if small else hc.hc_verify_keyed_quad
+    fn(_p(upk), ctypes.c_uint64(len(upk)), _p(kidx), _p(np.ascontiguousarray(sig)), _p(b),
+       _p(np.ascontiguousarray(off)), ctypes.c_uint64(n), _p(v))
     _, bad = counts(hc)
     assert bad == 0
     return v
 
 
-def test_keyed_quad_schedule_adversarial_bit_exact(hc, adversarial):
+@pytest.mark.parametrize('small', [False, True], ids=['4sides', '8sides'])
+def test_keyed_quad_schedule_adversarial_bit_exact(hc, adversarial, small):
     """Keyed latency kernel's schedule (k_verify_quad_keyed, pv_quad.h
-    q_keyed_side: each side's comb share on an emulated lane quad, -R added on
-    side 1, identity test): every adversarial case gives the fixture's verdict,
-    every multiply bound-checked."""
+    q_comb_side: each side's comb share on an emulated lane quad, -R added on
+    side 1, the sides' exchange tree, identity test; the hash wave's split
+    SHA-512), in both block forms (8 signatures x 4 sides; 4 x 8 for small
+    calls): every adversarial case gives the fixture's verdict, every multiply
+    bound-checked."""
     pk, sig, blob, off, want = _adv_arrays(adversarial)
-    v = _run_keyed_quad(hc, pk, sig, blob, off)
+    v = _run_keyed_quad(hc, pk, sig, blob, off, small)
     assert (v.astype(bool) == want).all()
 
 
-def test_keyed_quad_schedule_raw_vectors(hc, raw_vectors):
+@pytest.mark.parametrize('small', [False, True], ids=['4sides', '8sides'])
+def test_keyed_quad_schedule_raw_vectors(hc, raw_vectors, small):
     r = raw_vectors
     sel = slice(0, 600)
     pk, sig = r['pk'][sel], r['sig'][sel]
     off = r['off'][:601] - r['off'][0]
     blob = r['blob'][int(r['off'][0]):int(r['off'][600])]
-    v = _run_keyed_quad(hc, pk, sig, blob, off)
+    v = _run_keyed_quad(hc, pk, sig, blob, off, small)
     assert (v == r['verdict'][sel]).all()
 
 

@@ -307,10 +307,12 @@ void hc_verify_keyed_wide(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
 
 // keyed latency kernel (k_verify_quad_keyed): prepared keys, each of the
 // KQ_SIDES sides' comb share on an emulated quad, -R added on side 1, the
-// sides summed over the kernel's exchange tree (1 -> 0 and 3 -> 2, then 2 -> 0),
-// identity test on side 0
-void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
-                          const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* verdict) {
+// sides summed over the kernel's exchange tree (1 -> 0, 3 -> 2, ..., then 2 -> 0,
+// ..., then SIDES / 2 -> 0), identity test on side 0
+}  // extern "C" (a template below)
+template <int SIDES>
+static void verify_keyed_quad_t(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
+                                const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* verdict) {
   ensure_btab();
   uint32_t* ktab = (uint32_t*)calloc(k ? k * KEY_WORDS : KEY_WORDS, sizeof(uint32_t));
   uint32_t* scr = (uint32_t*)calloc(KEY_SCRATCH, sizeof(uint32_t));
@@ -328,24 +330,34 @@ void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
     keyed_record(rec, pre, dig);
     uint32_t nr[41];
     keyed_neg_r(nr, sig + 64 * i);
-    qfe eR, Q[KQ_SIDES], x;
+    qfe eR, Q[SIDES], x;
     q_load_cached(eR, nr, false, qr);
     const uint32_t* kt = ktab + (uint64_t)kidx[i] * KEY_WORDS;
-    for (int s = 0; s < KQ_SIDES; ++s) {
+    for (int s = 0; s < SIDES; ++s) {
       qfe hs, ls;
-      q_comb_base(hs, ls, sig + 64 * i, s, g_bw, qr);
-      q_comb_side(Q[s], rec, s, kt, hs, ls, qr);
+      q_comb_base<SIDES>(hs, ls, sig + 64 * i, s, g_bw, qr);
+      q_comb_side<SIDES>(Q[s], rec, s, kt, hs, ls, qr);
       q_keyed_add_negr(Q[s], eR, s, qr);
     }
-    for (int step = 1; step < KQ_SIDES / 2; step <<= 1)   // the kernel's shfl_xor 4 (step 1), 8 (step 2) ...
-      for (int s = 0; s < KQ_SIDES; s += 2 * step) {
+    for (int step = 1; step < SIDES / 2; step <<= 1)   // the kernel's shfl_xor 4 (step 1), 8 (step 2) ...
+      for (int s = 0; s < SIDES; s += 2 * step) {
         q_to_cached(x, Q[s + step], qr);
         q_add(Q[s], x, false, qr);
       }
-    q_to_cached(x, Q[KQ_SIDES / 2], qr);
+    q_to_cached(x, Q[SIDES / 2], qr);
     verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && nr[40] && q_sum_is_identity(Q[0], x, qr)) ? 1 : 0;
   }
   free(ktab);
+}
+extern "C" {
+void hc_verify_keyed_quad(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
+                          const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* verdict) {
+  verify_keyed_quad_t<KQ_SIDES>(pk, k, kidx, sig, blob, off, n, verdict);
+}
+// the small-call form: 4 signatures per block, KQ_SIDES_SMALL comb sides each
+void hc_verify_keyed_quad_small(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
+                                const uint8_t* blob, const uint64_t* off, uint64_t n, uint8_t* verdict) {
+  verify_keyed_quad_t<KQ_SIDES_SMALL>(pk, k, kidx, sig, blob, off, n, verdict);
 }
 
 // SHA-256(prefix || M_i) with the kernels' block loader; prefix < 0 = none
