@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
 
 // host-buffer (list) calls up to this size take the 4-signature blocks
 #ifndef KQ_SMALL_MAX
-#define KQ_SMALL_MAX 1024
+#define KQ_SMALL_MAX 256
 #endif
 hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uint8_t* sig, const uint8_t* blob,
                                     const uint64_t* off, uint64_t n, const uint32_t* list, const uint32_t* ktab,
