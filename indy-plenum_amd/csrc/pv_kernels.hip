@@ -558,6 +558,11 @@ hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_
   return hipGetLastError();
 }
 
+// small calls (signatures per launch): k_verify_quad's schedule lanes, the keyed
+// kernel's 4-signature blocks (host-buffer list calls)
+#ifndef KQ_SMALL_MAX
+#define KQ_SMALL_MAX 256
+#endif
 // PV_QUAD_PHASE (timing variants only, wrong verdicts): 1 skips the hash +
 // lattice wave, 2 the decompressions + tables, 3 the windows
 #ifndef PV_QUAD_PHASE
@@ -579,6 +584,10 @@ hipError_t launch_curve_lat(const uint8_t* pk, const uint8_t* sig, const uint32_
 // per call) run under the decompressions.  Verdict bits are stored as the
 // block's byte of the bitmap (8 signatures), so nothing needs zeroing; the
 // deferred count (pv_curve_stats) is added to *dcount (zeroed by the caller).
+// SCHED (calls up to KQ_SMALL_MAX signatures): the hash wave's message schedules
+// on their own lanes first, as in k_verify_quad_keyed (pv_quad.h keyed_hash);
+// larger calls keep hash_one (the 20 KB of schedules would halve the blocks per CU)
+template <bool SCHED>
 __global__ __launch_bounds__(128) void k_verify_quad(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
                                                      const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
                                                      uint64_t n, const uint32_t* __restrict__ bw,
@@ -587,6 +596,7 @@ __global__ __launch_bounds__(128) void k_verify_quad(const uint8_t* __restrict__
                                                      int force_full) {
   __shared__ uint32_t tabs[16 * QTAB_WORDS + PV_QUAD_LDS_PAD];
   __shared__ uint32_t recs[8 * HREC_WORDS];
+  __shared__ uint64_t kws[SCHED ? 80 * 8 * KQ_SCHED_BLOCKS : 1];
   const int t = (int)threadIdx.x;
   const uint64_t i0 = (uint64_t)blockIdx.x * 8;
   if (PV_QUAD_LDS_PAD && t == 0) tabs[16 * QTAB_WORDS] = 0;   // (keeps the padding allocated)
@@ -600,13 +610,28 @@ __global__ __launch_bounds__(128) void k_verify_quad(const uint8_t* __restrict__
     // wave 1: the scalar stage, lane k for signature i0 + k
     const int k = t - 64;
     uint32_t st = HS_NONE;
+    if constexpr (SCHED) {
+      const int sb = k & 7, bb = k >> 3;   // lane 8 b + s: block b's schedule of signature s
+      const uint64_t js = i0 + (uint64_t)sb;
+      if (bb < KQ_SCHED_BLOCKS && js < n && PV_QUAD_PHASE != 1) {
+        const uint64_t ml = off[js + 1] - off[js];
+        if ((uint64_t)bb < hram_blocks(ml))
+          keyed_sched_block(kws + k, 8 * KQ_SCHED_BLOCKS, sig + 64 * js, pk + 32 * js, blob + off[js], ml,
+                            (uint64_t)bb);
+      }
+      __threadfence_block();   // the schedules in LDS before the hashing lanes read them (same wave)
+      __builtin_amdgcn_wave_barrier();
+    }
     if (k < 8) {
       uint32_t* r = recs + HREC_WORDS * k;
       r[HREC_FLAGS] = HS_NONE;
       const uint64_t j = i0 + (uint64_t)k;
       if (j < n && PV_QUAD_PHASE != 1) {
         uint32_t dig[16];
-        const bool pre = hash_one(dig, pk + 32 * j, sig + 64 * j, blob + off[j], off[j + 1] - off[j]);
+        const uint64_t ml = off[j + 1] - off[j];
+        const bool pre = SCHED ? keyed_hash(dig, kws + k, 8 * KQ_SCHED_BLOCKS, 8, sig + 64 * j, pk + 32 * j,
+                                            blob + off[j], ml)
+                               : hash_one(dig, pk + 32 * j, sig + 64 * j, blob + off[j], ml);
         st = lattice_one(r, pre, dig, sig + 64 * j, force_full != 0);
       }
     }
@@ -649,8 +674,12 @@ hipError_t launch_verify_quad(const uint8_t* pk, const uint8_t* sig, const uint8
   const uint64_t blocks = (n + 7) / 8;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
   const uint64_t bytes = (n + 63) / 64 * 8;
-  hipLaunchKernelGGL(k_verify_quad, dim3((uint32_t)blocks), dim3(128), 0, s, pk, sig, blob, off, n, bw, verdict,
-                     reinterpret_cast<uint8_t*>(bitmap), bytes, dcount, force_full ? 1 : 0);
+  if (n <= KQ_SMALL_MAX)
+    hipLaunchKernelGGL(k_verify_quad<true>, dim3((uint32_t)blocks), dim3(128), 0, s, pk, sig, blob, off, n, bw,
+                       verdict, reinterpret_cast<uint8_t*>(bitmap), bytes, dcount, force_full ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_verify_quad<false>, dim3((uint32_t)blocks), dim3(128), 0, s, pk, sig, blob, off, n, bw,
+                       verdict, reinterpret_cast<uint8_t*>(bitmap), bytes, dcount, force_full ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -1071,10 +1100,6 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
   }
 }
 
-// host-buffer (list) calls up to this size take the 4-signature blocks
-#ifndef KQ_SMALL_MAX
-#define KQ_SMALL_MAX 256
-#endif
 hipError_t launch_verify_quad_keyed(const uint8_t* pk, bool pk_by_key, const uint8_t* sig, const uint8_t* blob,
                                     const uint64_t* off, uint64_t n, const uint32_t* list, const uint32_t* ktab,
                                     const uint32_t* kidx, const uint32_t* bw, uint8_t* verdict, uint64_t* bitmap,
