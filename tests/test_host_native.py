@@ -105,3 +105,39 @@ def test_pack_matches_python_packer():
     for bad in ([1, 2], [b'a', 'str'], [np.arange(6, dtype=np.uint8)[::2]], iter([b'a'])):
         with pytest.raises(_host.Fallback):
             _host.pack(bad)
+
+
+def test_verify_batch_call_path_passes_buffers_and_falls_back():
+    """_host.verify_batch (the wrapper's native call path into pv_verify_batch):
+    the five buffers reach the C function unchanged, n = the verdict length, the
+    mask / flags pass through, and a missing address or an unwritable verdict
+    buffer raises Fallback (the ctypes path then runs).  A stand-in C function
+    with pv_verify_batch's signature checks the arguments (no GPU)."""
+    import ctypes
+    import numpy as np
+    from plenum_gpu import _host
+    proto = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32)
+    seen = {}
+
+    def fake(pk, sig, blob, off, n, verdict, mask, flags):
+        seen.update(pk=pk, sig=sig, blob=blob, off=off, n=n, verdict=verdict, mask=mask, flags=flags)
+        ctypes.memset(verdict, 1, n)
+        return 7
+
+    cb = proto(fake)
+    addr = ctypes.cast(cb, ctypes.c_void_p).value
+    pk, sig = np.zeros((3, 32), np.uint8), np.zeros((3, 64), np.uint8)
+    blob, off = np.zeros(100, np.uint8), np.array([0, 10, 20, 30], np.uint64)
+    v = np.zeros(3, np.uint8)
+    rc = _host.verify_batch(addr, pk, sig, blob, off, v, 5, 2)
+    assert rc == 7 and (v == 1).all()
+    assert seen['pk'] == pk.ctypes.data and seen['sig'] == sig.ctypes.data and seen['blob'] == blob.ctypes.data
+    assert seen['off'] == off.ctypes.data and seen['verdict'] == v.ctypes.data
+    assert (seen['n'], seen['mask'], seen['flags']) == (3, 5, 2)
+    with pytest.raises(_host.Fallback):
+        _host.verify_batch(0, pk, sig, blob, off, v, 0, 0)
+    ro = np.zeros(3, np.uint8)
+    ro.flags.writeable = False
+    with pytest.raises(_host.Fallback):
+        _host.verify_batch(addr, pk, sig, blob, off, ro, 0, 0)
