@@ -911,8 +911,8 @@ hipError_t launch_keys_wide(const uint8_t* pk, uint64_t k, uint32_t* ktab, uint3
 // in cached form in LDS; the KQ_CW comb waves (16 lanes per signature:
 // KQ_SIDES = 4 lane quads, two comb tables and two base-point chunks each) sum
 // S's base-point chunks, then run the comb of h as soon as the record is there.
-// Side 1 then adds -R and the four sides' points are summed over two exchanges
-// (shfl_xor 4, then 8): side 0 tests the total for the identity.  One wave per
+// The sides' points are then summed over exchanges (shfl_xor 4, 8, ...) and side 0
+// tests the total plus -R for the identity.  One wave per
 // SIMD (four waves): no two paths share an issue port.
 // Round 5: four sides instead of two -- a comb lane's chain 28 (sq + mul) +
 // 2 x 34 mul -> 28 (sq + mul) + 2 x 20 mul + one more exchange level
@@ -1042,23 +1042,21 @@ __global__ __launch_bounds__(KQ_THREADS) void k_verify_quad_keyed(const uint8_t*
     const uint32_t* r = recs + KQ_WORDS * cs;
     kq_wait(ready);
     if (!(PV_KEYED_PHASE & 2)) q_comb_side<SIDES>(acc, r, side, kt, e_hi, e_lo, q);
-    kq_wait(ready + 1);
-    const uint32_t* nr = negr + KQ_NR * cs;
+    // the sides' sum before -R is needed: side s + 1 -> s for even s (xor 4), then
+    // side 2 -> 0 (xor 8) ..., so that only one add-and-test follows the root
+    // wave's flag (round 5: the root chain is the longer path)
     qfe eR, x, xo;
-    q_load_cached(eR, nr, false, q);
-    q_keyed_add_negr(acc, eR, side, q);
-    // the sides' sum: side s + 1 -> s for even s (xor 4), then side 2 -> 0 (xor 8) ...
 #pragma unroll
-    for (int step = 1; step < SIDES / 2; step <<= 1) {
+    for (int step = 1; step < SIDES; step <<= 1) {
       q_to_cached(x, acc, q);
 #pragma unroll
       for (int i = 0; i < 10; ++i) xo.l[0].v[i] = __shfl_xor(x.l[0].v[i], 4 * step, 64);
       q_add(acc, xo, false, q);   // meaningful on sides s % (2 step) == 0; the others compute alike, unused
     }
-    q_to_cached(x, acc, q);
-#pragma unroll
-    for (int i = 0; i < 10; ++i) xo.l[0].v[i] = __shfl_xor(x.l[0].v[i], 2 * SIDES, 64);   // side S/2 -> 0
-    const bool id = q_sum_is_identity(acc, xo, q);
+    kq_wait(ready + 1);
+    const uint32_t* nr = negr + KQ_NR * cs;
+    q_load_cached(eR, nr, false, q);
+    const bool id = q_sum_is_identity(acc, eR, q);   // R' + (-R) = O on side 0
     const bool v = r[KQ_OK] != 0 && kt[KEY_STATUS] != 0 && nr[40] != 0 && id;
     const bool mine = side == 0 && (t & 3) == 0 && e < n;
     if (mine) verdict[ic] = v ? 1 : 0;

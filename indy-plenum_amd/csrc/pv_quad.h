@@ -418,7 +418,7 @@ PV_HD bool q_sum_is_identity(const qfe& Q0, const qfe& e1, const QRole& q) {
 // hc_verify_keyed_quad on the host).  libsodium accepts iff
 // encode(R') == R, i.e. iff R decodes with a canonical y and R' + (-R) = O (the
 // identity test of the half-size path, pv_lattice.h): -R is decoded while the
-// scalar wave hashes, side 1 adds it, and side 0 tests the total for O.
+// scalar wave hashes, and side 0 tests the sides' total plus -R for O.
 //
 // record (LDS): h + the radix-16 digit offsets (8 words), pre-check verdict
 constexpr int KQ_H = 0, KQ_OK = 8, KQ_WORDS = 9;
@@ -539,21 +539,6 @@ PV_HD void q_comb_side(qfe& acc, const uint32_t* rec, int side, const uint32_t* 
     if (w == 4) q_add(acc, e_hi, false, q);
   }
   q_add(acc, e_lo, false, q);
-}
-
-// side 1 adds -R (eR: -R in cached add order, q_load_cached); the other sides
-// add the identity: the same instruction stream on every quad
-PV_HD void q_keyed_add_negr(qfe& acc, const qfe& eR, int side, const QRole& q) {
-  const uint32_t sm = 0u - (uint32_t)(side == 1);
-  qfe e;
-#pragma unroll
-  for (int j = 0; j < QL; ++j) {
-    fe id;
-    role_cached_identity(id, qrole(j, q));
-#pragma unroll
-    for (int i = 0; i < 10; ++i) e.l[j].v[i] = bitsel(sm, eR.l[j].v[i], id.v[i]);
-  }
-  q_add(acc, e, false, q);
 }
 
 // -R of the keyed verdict as k_verify_quad_keyed's decoding lane leaves it:

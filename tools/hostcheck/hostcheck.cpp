@@ -306,9 +306,9 @@ void hc_verify_keyed_wide(const uint8_t* pk, uint64_t k, const uint32_t* kidx, c
 }
 
 // keyed latency kernel (k_verify_quad_keyed): prepared keys, each of the
-// KQ_SIDES sides' comb share on an emulated quad, -R added on side 1, the
-// sides summed over the kernel's exchange tree (1 -> 0, 3 -> 2, ..., then 2 -> 0,
-// ..., then SIDES / 2 -> 0), identity test on side 0
+// SIDES sides' comb share on an emulated quad, the sides summed over the
+// kernel's exchange tree (1 -> 0, 3 -> 2, ..., then 2 -> 0, ..., then SIDES / 2
+// -> 0), the total plus -R tested for the identity on side 0
 }  // extern "C" (a template below)
 template <int SIDES>
 static void verify_keyed_quad_t(const uint8_t* pk, uint64_t k, const uint32_t* kidx, const uint8_t* sig,
@@ -337,15 +337,13 @@ static void verify_keyed_quad_t(const uint8_t* pk, uint64_t k, const uint32_t* k
       qfe hs, ls;
       q_comb_base<SIDES>(hs, ls, sig + 64 * i, s, g_bw, qr);
       q_comb_side<SIDES>(Q[s], rec, s, kt, hs, ls, qr);
-      q_keyed_add_negr(Q[s], eR, s, qr);
     }
-    for (int step = 1; step < SIDES / 2; step <<= 1)   // the kernel's shfl_xor 4 (step 1), 8 (step 2) ...
+    for (int step = 1; step < SIDES; step <<= 1)   // the kernel's shfl_xor 4 (step 1), 8 (step 2) ...
       for (int s = 0; s < SIDES; s += 2 * step) {
         q_to_cached(x, Q[s + step], qr);
         q_add(Q[s], x, false, qr);
       }
-    q_to_cached(x, Q[SIDES / 2], qr);
-    verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && nr[40] && q_sum_is_identity(Q[0], x, qr)) ? 1 : 0;
+    verdict[i] = (rec[KQ_OK] && kt[KEY_STATUS] && nr[40] && q_sum_is_identity(Q[0], eR, qr)) ? 1 : 0;
   }
   free(ktab);
 }
