@@ -134,6 +134,30 @@ def _pmc(path, key):
         return None
 
 
+def _key_prep_roofline(batch, config, peak, reps=3):
+    """k_keys (the narrow-format key preparation of a keyed step) priced like the
+    curve: W_MAD_KEYPREP per distinct key / its HIP-event duration on the launch
+    stream (pv_keys_prepare_device runs on torch's current stream), after the
+    timed region; HBM bytes per launch from the committed PMC profile (C4)."""
+    k = int(batch.keys[0].shape[0])
+    batch.prepare_keys()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        batch.prepare_keys()
+    b.record()
+    b.synchronize()
+    ms = a.elapsed_time(b) / reps
+    work = (W_MUL_KEYPREP * 100 + W_SQ_KEYPREP * 55) * k
+    traffic = _pmc(KEYED_PMC[config], 'key_prep_hbm_bytes_per_launch') if config == 'c4' else None
+    return {'kernel': 'k_keys', 'keys': k, 'ms': round(ms, 4), 'achieved': round(work / (ms * 1e-3) / 1e12, 3),
+            'peak': round(peak / 1e12, 3), 'frac': round(work / (ms * 1e-3) / peak, 4),
+            'traffic': round(traffic * k / (1 << 20)) if traffic else None,
+            'note': 'W_MAD_KEYPREP = {} v_mad lane-ops per key (host op count) / HIP-event duration, {} '
+                    'launches after the timed region; traffic: PMC FETCH+WRITE of the C4 launch '
+                    '(2^20 keys) scaled per key'.format(int(W_MUL_KEYPREP * 100 + W_SQ_KEYPREP * 55), reps)}
+
+
 def _traffic_per_launch(config='c2', n=None):
     """HBM bytes per curve launch of the config's full-size line from the committed
     rocprofv3 PMC summary (C2: r05_curve_pmc.json; C3 / C4: the keyed curve launch
@@ -1027,6 +1051,9 @@ def main():
     achieved = work / (ms_curve * 1e-3)
     achieved_step = work / (ms_step * 1e-3)
     peak = _mad_peak()
+    key_prep = None
+    if key_cache and not batch.wide:
+        key_prep = _key_prep_roofline(batch, args.config, peak)
 
     total = world * n * args.steps
     value = total / elapsed
@@ -1056,6 +1083,7 @@ def main():
                                   'note': 'curve MAD work per step / per-step time of the timed region (every kernel '
                                           'of the step charged to the curve)'},
                      'traffic': traffic,
+                     'key_prep': key_prep,
                      'work_per_verify': wpv,
                      'combined_issue': _combined_issue(n / (ms_curve * 1e-3), peak)
                      if (args.config, n) == ('c2', CONFIGS['c2']['n']) and curve_mode == 'half' else None},
