@@ -802,7 +802,8 @@ def other_configs():
         r['workload'] = (line.get('config') or {}).get('workload')
         rf = line.get('roofline') or {}
         if rf:
-            r['roofline'] = {k: rf.get(k) for k in ('kernel', 'achieved', 'peak', 'unit', 'frac', 'traffic')}
+            r['roofline'] = {k: rf.get(k) for k in ('kernel', 'achieved', 'peak', 'unit', 'frac', 'traffic', 'key_prep')
+                             if k != 'key_prep' or rf.get(k)}
         r['child_wall_s'] = round(time.perf_counter() - t0, 2)
         res[name] = r
     return res
