@@ -68,6 +68,11 @@ PV_HD bool ge8(const uint32_t a[8], const uint32_t b[8]) {
 }
 
 PV_HD void add8(uint32_t a[8], const uint32_t b[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = __builtin_addc(a[k], b[k], c, &c);
+#else
   uint64_t c = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -75,9 +80,15 @@ PV_HD void add8(uint32_t a[8], const uint32_t b[8]) {
     a[k] = (uint32_t)c;
     c >>= 32;
   }
+#endif
 }
 
 PV_HD void sub8(uint32_t a[8], const uint32_t b[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned bw = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = __builtin_subc(a[k], b[k], bw, &bw);
+#else
   uint32_t br = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -85,11 +96,34 @@ PV_HD void sub8(uint32_t a[8], const uint32_t b[8]) {
     a[k] = (uint32_t)d;
     br = (uint32_t)(d >> 63);
   }
+#endif
 }
 
 // a -= q b over 8 words; returns true iff the exact result is negative (then a
 // holds it mod 2^256; callers know it lies in (-b, 0))
 PV_HD bool submul8(uint32_t a[8], const uint32_t b[8], uint32_t q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // device: the eight products q b_k are independent (one v_mad_u64_u32 each);
+  // their low words and the previous product's high word leave a[k] through two
+  // borrow chains (v_subb_co_u32 with carry in/out) instead of 64-bit sign tricks
+  uint32_t lo[8], hi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t p = (uint64_t)q * b[k];
+    lo[k] = (uint32_t)p;
+    hi[k] = (uint32_t)(p >> 32);
+  }
+  unsigned b1 = 0, b2 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    unsigned o1, o2;
+    const uint32_t t = __builtin_subc(a[k], lo[k], b1, &o1);
+    a[k] = __builtin_subc(t, k ? hi[k - 1] : 0u, b2, &o2);
+    b1 = o1;
+    b2 = o2;
+  }
+  return (hi[7] | b1 | b2) != 0;
+#else
   uint64_t pc = 0;
   uint32_t br = 0;
 #pragma unroll
@@ -101,10 +135,27 @@ PV_HD bool submul8(uint32_t a[8], const uint32_t b[8], uint32_t q) {
     br = (uint32_t)(d >> 63);
   }
   return (pc + br) != 0;
+#endif
 }
 
 // t += q u (HS_T words; no overflow by the bounds above)
 PV_HD void addmul_t(uint32_t t[HS_T], const uint32_t u[HS_T], uint32_t q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // independent products, their low and (shifted) high words added by two carry chains
+  uint32_t lo[HS_T], hi[HS_T];
+#pragma unroll
+  for (int k = 0; k < HS_T; ++k) {
+    const uint64_t p = (uint64_t)q * u[k];
+    lo[k] = (uint32_t)p;
+    hi[k] = (uint32_t)(p >> 32);
+  }
+  unsigned c1 = 0, c2 = 0;
+#pragma unroll
+  for (int k = 0; k < HS_T; ++k) {
+    const uint32_t x = __builtin_addc(t[k], lo[k], c1, &c1);
+    t[k] = __builtin_addc(x, k ? hi[k - 1] : 0u, c2, &c2);
+  }
+#else
   uint64_t c = 0;
 #pragma unroll
   for (int k = 0; k < HS_T; ++k) {
@@ -112,9 +163,15 @@ PV_HD void addmul_t(uint32_t t[HS_T], const uint32_t u[HS_T], uint32_t q) {
     t[k] = (uint32_t)p;
     c = p >> 32;
   }
+#endif
 }
 
 PV_HD void add_t(uint32_t t[HS_T], const uint32_t u[HS_T]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned cc = 0;
+#pragma unroll
+  for (int k = 0; k < HS_T; ++k) t[k] = __builtin_addc(t[k], u[k], cc, &cc);
+#else
   uint64_t c = 0;
 #pragma unroll
   for (int k = 0; k < HS_T; ++k) {
@@ -122,9 +179,15 @@ PV_HD void add_t(uint32_t t[HS_T], const uint32_t u[HS_T]) {
     t[k] = (uint32_t)c;
     c >>= 32;
   }
+#endif
 }
 
 PV_HD void sub_t(uint32_t t[HS_T], const uint32_t u[HS_T]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned bw = 0;
+#pragma unroll
+  for (int k = 0; k < HS_T; ++k) t[k] = __builtin_subc(t[k], u[k], bw, &bw);
+#else
   uint32_t br = 0;
 #pragma unroll
   for (int k = 0; k < HS_T; ++k) {
@@ -132,6 +195,7 @@ PV_HD void sub_t(uint32_t t[HS_T], const uint32_t u[HS_T]) {
     t[k] = (uint32_t)d;
     br = (uint32_t)(d >> 63);
   }
+#endif
 }
 
 // One exact Euclid step (ra >= rb > 0): q = floor(ra / rb),
