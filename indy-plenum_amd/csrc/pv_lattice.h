@@ -202,8 +202,23 @@ PV_HD void sub_t(uint32_t t[HS_T], const uint32_t u[HS_T]) {
 // (ra, ta) <- (ra - q rb, ta + q tb).  q is estimated in float64 (within one
 // of the true quotient while q < 2^32) and fixed by one conditional add or
 // subtract of rb.  false: quotient too large for one 32-bit step (deferred).
+// floor(a / b) within one: the device takes the hardware reciprocal and two
+// Newton steps (relative error ~2^-50, so below 2^-18 absolute while the
+// quotient is < 2^32) instead of the correctly rounded division sequence; the
+// callers correct the quotient by one either way
+PV_HD double quot_est(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(r, fma(-b, r, 1.0), r);
+  r = fma(r, fma(-b, r, 1.0), r);
+  return floor(a * r);
+#else
+  return floor(a / b);
+#endif
+}
+
 PV_HD bool euclid_step(uint32_t ra[8], uint32_t ta[HS_T], const uint32_t rb[8], const uint32_t tb[HS_T]) {
-  const double qd = floor(words_to_f64(ra) / words_to_f64(rb));
+  const double qd = quot_est(words_to_f64(ra), words_to_f64(rb));
   if (!(qd < 4294967294.0)) return false;
   const uint32_t q = (uint32_t)qd;
   if (submul8(ra, rb, q)) {          // over-estimate by one
