@@ -1,6 +1,6 @@
 """Bench: Ed25519 verifies/s on MI355X (BASELINE.json metric, config C2).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]          (N > 1: starts the N ranks itself)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -10,10 +10,19 @@ signed requests (distinct keys, 256 B payloads, ~5 % tampered) that is already
 resident in HBM, plus — when N > 1 — the RCCL all-gather of every rank's
 packed verdict bitmap.  Weak scaling: each rank owns a disjoint index range.
 
+`--gpus N` means N GPUs whichever way the script is started: under
+torch.distributed.run (WORLD_SIZE set) it must equal WORLD_SIZE; started
+directly with N > 1 it launches the N rank processes itself (fresh children,
+created before this process makes any GPU call, one per GPU, RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT) and exits with their
+status.  N larger than the visible GPU count is refused (exit 2) unless the
+ranks share GPU 0 (PV_BENCH_SHARE_GPU=1, the gloo rehearsal).
+
 Rank 0 prints ONE JSON line.  `value` = all ranks' verifies / max-over-ranks
 time.  `roofline` prices the dominant (curve) kernel against the measured
 v_mad_u64_u32 issue rate; `cpu_baseline` times libsodium 1.0.18 (the native
-call under Plenum's Verifier.verify) on the host cores, rank 0, N = 1 only.
+call under Plenum's Verifier.verify) on the host cores, on rank 0 after the
+timed region and the final barrier (every N).
 """
 import argparse
 import ctypes
@@ -809,9 +818,100 @@ def other_configs():
     return res
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(('127.0.0.1', 0))
+        return so.getsockname()[1]
+
+
+def _visible_gpus():
+    """GPUs this process may use, counted without initialising HIP
+    (torch.cuda.device_count() does not create a context on this image)."""
+    try:
+        return torch.cuda.device_count()
+    except Exception:   # noqa: BLE001 - no runtime: no GPUs
+        return 0
+
+
+def rank_plan(gpus, environ=None, visible=None):
+    """How `bench.py --gpus N` runs, decided before any GPU call:
+    -> ('error', message) | ('launch', N) (start N rank children) |
+       ('run', world) (this process is a rank, or the only one).
+    `gpus` None = the launcher's WORLD_SIZE (or 1)."""
+    environ = os.environ if environ is None else environ
+    share = environ.get('PV_BENCH_SHARE_GPU') == '1'
+    ws = environ.get('WORLD_SIZE')
+    if ws is not None:
+        try:
+            world = int(ws)
+        except ValueError:
+            return 'error', 'WORLD_SIZE={!r} is not an integer'.format(ws)
+        if gpus is not None and gpus != world:
+            return 'error', ('--gpus {} but WORLD_SIZE={} (the launcher started {} ranks): run it with '
+                             '--gpus {}'.format(gpus, world, world, world))
+        n = world
+    else:
+        n = 1 if gpus is None else gpus
+    if n < 1:
+        return 'error', '--gpus must be >= 1 (got {})'.format(n)
+    if n > 1 and not share:
+        vis = _visible_gpus() if visible is None else visible
+        if n > vis:
+            return 'error', ('--gpus {} but only {} GPU(s) are visible (PV_BENCH_SHARE_GPU=1 runs every rank on '
+                             'GPU 0 for a rehearsal)'.format(n, vis))
+    if ws is None and n > 1:
+        return 'launch', n
+    return 'run', n
+
+
+def launch_ranks(n, argv):
+    """Start ranks 0..n-1 as fresh child processes of this script (same argv,
+    --gpus n), each with the torch.distributed env of one rank on GPU `rank`.
+    stdout / stderr are inherited: rank 0 alone prints the JSON line.  When a
+    rank fails, the others get SIGTERM (exact PIDs) after a grace period, so a
+    peer stuck in a collective cannot outlive the job.  -> exit status."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'),
+                   PV_BENCH_LAUNCHER='self')
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__)] + argv, env=env, cwd=REPO))
+    rcs = [None] * n
+    failed_at = None
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0, 3) and failed_at is None:
+                    failed_at = time.monotonic()
+                    print('bench.py: rank {} exited with {}'.format(r, rcs[r]), file=sys.stderr, flush=True)
+        if failed_at is not None and time.monotonic() - failed_at > 30:
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    try:
+                        rcs[r] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[r] = p.wait()
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc not in (0, 3)]
+    if bad:
+        return bad[0] if bad[0] > 0 else 1
+    return 3 if 3 in rcs else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None,
+                    help='GPUs (ranks); default: WORLD_SIZE under a launcher, else 1.  N > 1 without a launcher '
+                         'starts the N ranks itself')
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', choices=sorted(CONFIGS) + ['f3', 'c3bls'], default='c2',
@@ -836,6 +936,21 @@ def main():
                     help='one stream, each step after the previous one (default: consecutive steps alternate over '
                          'two streams and two workspaces, so step k + 1 starts while step k\'s curve grid drains)')
     args = ap.parse_args()
+    # --gpus N means N ranks: decided before this process touches the GPU (a
+    # self-launch starts fresh children; no exec from a process with a context)
+    action, nranks = rank_plan(args.gpus)
+    if action == 'error':
+        print('bench.py: ' + nranks, file=sys.stderr, flush=True)
+        return 2
+    if action == 'launch':
+        argv = sys.argv[1:]
+        if args.gpus is None:
+            argv += ['--gpus', str(nranks)]
+        return launch_ranks(nranks, argv)
+    if nranks > 1 and args.config in ('c1', 'c3bls', 'f3'):
+        print('bench.py: --config {} is a one-GPU line (no sharded path); run it with --gpus 1'.format(args.config),
+              file=sys.stderr, flush=True)
+        return 2
     # PV_* schedule knobs (A/B runs of tools/*.sh): an explicit opt-in here --
     # the library never reads the environment; a non-default setting is
     # reported in the line
@@ -1003,10 +1118,23 @@ def main():
             dist.all_reduce(cks[0], op=dist.ReduceOp.MIN)
             dist.all_reduce(cks[1], op=dist.ReduceOp.MAX)
             mism += int(cks[0].item() != cks[1].item())
+    ranks = None
     if coll:
         m = coll_dev(torch.tensor([mism], dtype=torch.int64, device=dev))
         dist.all_reduce(m)
         mism = int(m.item())
+        # which GPU every rank ran on (HIP ordinal + PCI bus id), gathered
+        props = torch.cuda.get_device_properties(dev)
+        mine = torch.tensor([rank, dev.index, int(getattr(props, 'pci_bus_id', -1) or -1)], dtype=torch.int64,
+                            device=dev)
+        allr = torch.zeros(world * 3, dtype=torch.int64, device=dev)
+        all_gather(allr, mine)
+        ranks = {'world_size': dist.get_world_size(), 'backend': dist.get_backend(),
+                 'launcher': os.environ.get('PV_BENCH_LAUNCHER', 'external (torch.distributed.run)'),
+                 'devices': [{'rank': int(a), 'device': int(b), 'pci_bus_id': int(c)}
+                             for a, b, c in allr.view(world, 3).cpu().tolist()]}
+        if ranks['world_size'] != world:
+            mism += 1
 
     # kernel-level timing for the roofline: HIP events on the launch stream,
     # recorded during the timed steps above (averaged over those launches)
@@ -1099,7 +1227,13 @@ def main():
         out['config']['quorum'] = tally['q']
         out['batches_per_s'] = round(world * tally['nb'] * args.steps / elapsed, 1)
         out['quorum_reached'] = int(tally['reached'][0].sum().item())
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if ranks is not None:
+        out['ranks'] = ranks
+    if coll:
+        # every rank has finished its timed region and checks: rank 0 prices the
+        # host baseline while the others wait at the closing barrier
+        dist.barrier()
+    if rank == 0 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(batch, args.config.upper())
     if world == 1 and args.config == 'c2' and not args.no_e2e:
         out['end_to_end'] = end_to_end(batch, key_cache)

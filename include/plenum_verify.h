@@ -91,6 +91,12 @@ void pv_shutdown(void);
  * that no device is initialised (PV_EINVAL otherwise); pv_shutdown ends it. */
 int pv_test_init_dup(uint32_t k);
 
+/* TEST ONLY: the spin budget (ns, default 20,000,000) a zero-copy small call
+ * polls its completion word for before it falls back to hipStreamSynchronize;
+ * 0 sends every such call through the fallback (tests/test_gpu_latency.py).
+ * PV_EINVAL for ns < 0. */
+int pv_test_set_spin_ns(int64_t ns);
+
 /* Human-readable description of the last error on this thread ("" if none). */
 const char *pv_last_error(void);
 

@@ -895,10 +895,14 @@ uint64_t small_bytes(const HostBatch& hb, uint64_t s, uint64_t e) {
 #ifndef PV_ZC_POLL
 #define PV_ZC_POLL 1
 #endif
-// all-cached zero-copy calls up to this size complete by the keyed kernel's own word
-constexpr uint64_t ZC_SELF_MAX = 128;
+// all-cached zero-copy calls up to this size complete by the keyed kernel's own
+// word: 64 signatures = the 16 blocks of 4 that profiles/r05_ab_completion_word.jsonl
+// measured faster than a k_signal launch (125 blocks measured slower)
+constexpr uint64_t ZC_SELF_MAX = 64;
+// spin budget of the completion word before the stream synchronize takes over
+// (pv_test_set_spin_ns shortens it so a test reaches the fallback)
+std::atomic<int64_t> g_zc_spin_ns{20'000'000};
 // spins until *w == v (acquire) or `ns` nanoseconds have passed
-constexpr int64_t ZC_SPIN_NS = 20'000'000;
 bool spin_wait_word(const uint32_t* w, uint32_t v, int64_t ns) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t i = 0;; ++i) {
@@ -980,7 +984,15 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
   uint32_t seq = 0;
   bool signalled = false;
   if (poll) {
+    const bool fresh = d.zc_flag.p == nullptr;
     HIP_OK(d.zc_flag.ensure(64));
+    // hipHostMalloc leaves the contents unspecified (recycled pinned pages after a
+    // shutdown / init cycle): a stale word equal to the first seq would complete
+    // the call before the kernel ran
+    if (fresh) {
+      __atomic_store_n(reinterpret_cast<uint32_t*>(d.zc_flag.p), 0u, __ATOMIC_RELEASE);
+      d.zc_seq = 0;
+    }
     if (++d.zc_seq == 0) d.zc_seq = 1;
     seq = d.zc_seq;
   }
@@ -1020,7 +1032,8 @@ int run_small(Device& d, const HostBatch& hb, uint64_t s, uint64_t e) {
     // past the spin budget (a fault, a long queue) the synchronize reports /
     // waits as before
     if (!signalled) HIP_OK(pv::launch_signal(reinterpret_cast<uint32_t*>(d.zc_flag.dev), seq, w.stream));
-    drain.done = spin_wait_word(reinterpret_cast<const uint32_t*>(d.zc_flag.p), seq, ZC_SPIN_NS);
+    drain.done = spin_wait_word(reinterpret_cast<const uint32_t*>(d.zc_flag.p), seq,
+                                 g_zc_spin_ns.load(std::memory_order_relaxed));
     if (!drain.done) HIP_OK(hipStreamSynchronize(w.stream));
   } else {
     if (!zc) HIP_OK(hipMemcpyAsync(vout.p, d.verdict.p, m, hipMemcpyDeviceToHost, w.stream));
@@ -1367,6 +1380,12 @@ int pv_test_init_dup(uint32_t k) {
   const int rc = init_devices(0, g_dup);
   if (rc != PV_OK) g_dup = 0;
   return rc;
+}
+
+int pv_test_set_spin_ns(int64_t ns) {
+  if (ns < 0) return fail(PV_EINVAL, "pv_test_set_spin_ns: ns must be >= 0 (got %lld)", (long long)ns);
+  g_zc_spin_ns.store(ns, std::memory_order_relaxed);
+  return PV_OK;
 }
 
 void pv_shutdown(void) {

@@ -812,7 +812,7 @@ int pv_bls_add_keys(const uint8_t* pks, uint64_t k, uint8_t* status, uint64_t* f
   if (!ks.gen_ok)
     return bfail(PV_ENOTINIT, "no BLS key set on device %d (call pv_bls_set_keys)", device);
   const uint64_t old = ks.nkeys;
-  if (old + k > 65535)
+  if (old > 65535 || k > 65535 - old)   // no wrap for any k
     return bfail(PV_EINVAL, "at most 65535 keys per set (%llu + %llu)", (unsigned long long)old,
                  (unsigned long long)k);
   if (first) *first = old;

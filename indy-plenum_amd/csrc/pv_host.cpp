@@ -364,6 +364,17 @@ PyObject* verify_batch(PyObject*, PyObject* args) {
     return fallback();
   }
   const uint64_t n = (uint64_t)b[4].len;   // one verdict byte per signature
+  // every input must cover n signatures and off[n] the blob: a caller that skipped
+  // the Python shape checks gets the ValueError of the ctypes path, never a read
+  // past a buffer with the GIL released
+  const uint64_t* offp = static_cast<const uint64_t*>(b[3].buf);
+  const bool sized = (uint64_t)b[0].len >= 32 * n && (uint64_t)b[1].len >= 64 * n &&
+                     (uint64_t)b[3].len >= 8 * (n + 1) && offp[n] <= (uint64_t)b[2].len;
+  if (!sized) {
+    for (int i = 0; i < 5; ++i) PyBuffer_Release(&b[i]);
+    PyErr_SetString(PyExc_ValueError, "verify_batch: pk / sig / off / blob smaller than the verdict count needs");
+    return nullptr;
+  }
   int rc;
   Py_BEGIN_ALLOW_THREADS
   rc = reinterpret_cast<verify_fn>((uintptr_t)fn)(static_cast<const uint8_t*>(b[0].buf),

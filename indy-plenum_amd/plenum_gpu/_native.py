@@ -25,6 +25,7 @@ SIGNATURES = [
     ('pv_init', ctypes.c_int, [ctypes.c_uint32]),
     ('pv_shutdown', None, []),
     ('pv_test_init_dup', ctypes.c_int, [ctypes.c_uint32]),
+    ('pv_test_set_spin_ns', ctypes.c_int, [ctypes.c_int64]),
     ('pv_last_error', ctypes.c_char_p, []),
     ('pv_device_count', ctypes.c_int, []),
     ('pv_verify_batch', ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, ctypes.c_uint32]),
@@ -366,10 +367,18 @@ def test_init_dup(k):
         _inited_mask = 0
 
 
+def test_set_spin_ns(ns):
+    """TEST ONLY: pv_test_set_spin_ns -- the completion-word spin budget of
+    zero-copy small calls (0: every such call takes the synchronize fallback)."""
+    _check('pv_test_set_spin_ns', load().pv_test_set_spin_ns(int(ns)))
+
+
 def shutdown():
     global _inited_mask
     with _lock:
         _cached_keys.clear()
+        # pv_bls_shutdown releases every device key set: the content index must go too
+        _bls_sets.clear()
         if _lib is not None:
             _lib.pv_shutdown()
             _lib.pv_bls_shutdown()
@@ -578,6 +587,8 @@ def bls_key_indices(gen, pks, device=0):
     gen = bytes(gen)
     with _lock:
         ks = _bls_sets.get(device)
+    if ks is not None and ks.gen == gen and bls_keyset_info(device)[0] < len(ks.status):
+        ks = None   # the device set was released behind this index (pv_bls_shutdown): rebuild it
     if ks is None or ks.gen != gen:
         new = list(dict.fromkeys(pks))
         bls_set_keys(gen, np.frombuffer(b''.join(new), np.uint8) if new else np.zeros((0, 128), np.uint8),

@@ -227,3 +227,22 @@ def test_commit_batch_and_quorum(fx, nat):
     assert list(votes) == [nn - k for k in n_bad]
     assert list(reached) == [nn - k >= q.commit.value for k in n_bad]
     assert 0 < sum(reached) < nb
+
+
+def test_verify_after_shutdown_reinit(fx, nat):
+    """shutdown() releases the device key set (pv_bls_shutdown); the content
+    index of the key set must go with it, so a verifier built after re-init with
+    the same generator rebuilds the set instead of trusting stale indices
+    (ADVICE r5).  Also: a set released behind the index (pv_bls_shutdown called
+    directly) is detected through pv_bls_keyset_info and rebuilt."""
+    from plenum_gpu.bls import (BlsCryptoVerifierGpu, BlsGroupParamsLoaderIndyCrypto, IndyCryptoBlsUtils, VerKey)
+    c = next(c for c in fx['cases'] if c['verdict'] and 'key' in c)
+    item = (IndyCryptoBlsUtils.bls_to_str(VerKey(bytes.fromhex(c['sig']))), bytes.fromhex(c['msg']),
+            VerKey(bytes.fromhex(fx['keys'][c['key']]['pk'])))
+    params = BlsGroupParamsLoaderIndyCrypto().load_group_params()
+    assert BlsCryptoVerifierGpu(params).verify_sig(*item) is True
+    nat.shutdown()
+    nat.ensure_init()
+    assert BlsCryptoVerifierGpu(params).verify_sig(*item) is True
+    nat.load().pv_bls_shutdown()
+    assert BlsCryptoVerifierGpu(params).verify_sig(*item) is True

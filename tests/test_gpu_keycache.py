@@ -175,3 +175,26 @@ def test_completion_word_over_many_calls(nat, raw_vectors):
             start = int(rng.integers(1500, len(want) - n + 1))
         got = nat.verify_batch_arrays(*_slice(r, start, n))
         assert (got == want[start:start + n]).all(), (c, kind, start, n)
+
+
+def test_completion_word_synchronize_fallback(nat, raw_vectors):
+    """With no spin budget (pv_test_set_spin_ns(0)) every zero-copy call gives up
+    on its completion word and reaches the hipStreamSynchronize fallback; the
+    verdicts must still be the fixture's, for the kernel-written word (all keys
+    cached) and the k_signal word (mixed / uncached), and a later call with the
+    default budget must not see a stale word from the fallback calls."""
+    r = raw_vectors
+    want = r['verdict'].astype(bool)
+    nat.keycache_add(r['pk'][:1500])
+    try:
+        nat.test_set_spin_ns(0)
+        for start, n in ((0, 1), (3, 64), (1490, 20), (2000, 9), (1700, 1000)):
+            got = nat.verify_batch_arrays(*_slice(r, start, n))
+            assert (got == want[start:start + n]).all(), ('fallback', start, n)
+    finally:
+        nat.test_set_spin_ns(20_000_000)
+    for start, n in ((5, 8), (2100, 7)):
+        got = nat.verify_batch_arrays(*_slice(r, start, n))
+        assert (got == want[start:start + n]).all(), ('after', start, n)
+    with pytest.raises(Exception):
+        nat.test_set_spin_ns(-1)

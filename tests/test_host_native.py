@@ -141,3 +141,10 @@ def test_verify_batch_call_path_passes_buffers_and_falls_back():
     ro.flags.writeable = False
     with pytest.raises(_host.Fallback):
         _host.verify_batch(addr, pk, sig, blob, off, ro, 0, 0)
+    # undersized inputs: ValueError before the C function is reached
+    seen.clear()
+    for args in ((pk[:2], sig, blob, off), (pk, sig[:2], blob, off), (pk, sig, blob, off[:3]),
+                 (pk, sig, blob[:29], off)):
+        with pytest.raises(ValueError):
+            _host.verify_batch(addr, *args, v, 0, 0)
+    assert not seen
