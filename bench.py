@@ -203,6 +203,87 @@ W_FULL_PER_VERIFY = (FULL_COST['mul'] * W_MUL_PER_VERIFY + FULL_COST['sq'] * W_S
                      + 3 * W_SQ2X_PER_VERIFY)
 
 
+# k_hash: one SHA-512 compression of R||A||M per 128-byte block, as pv_sha512.h
+# writes it in its minimal gfx950 form.  Per block, by
+# instruction: 80 rounds x (Sigma0, Sigma1: 3 64-bit rotates = 6 v_alignbit_b32
+# each; Sigma xors, Ch, Maj: 2 v_bitop3_b32 each; 7 64-bit adds incl. K + W as
+# v_lshl_add_u64) + 64 schedule words x (sigma0, sigma1: 2 rotates + a shift =
+# 5 v_alignbit_b32 + 1 v_lshrrev_b32 each, 2 v_bitop3_b32 each; 3 64-bit adds)
+# + the 8 state adds + the big-endian decode of 16 words (2 v_perm_b32 each).
+SHA_W_PER_BLOCK = {'v_alignbit_b32': 80 * 12 + 64 * 10, 'v_bitop3_b32': 80 * 8 + 64 * 4,
+                   'v_lshl_add_u64': 80 * 7 + 64 * 3 + 8, 'v_lshrrev_b32': 64 * 2, 'v_perm_b32': 32}
+SHA_INSN_PER_BLOCK = sum(SHA_W_PER_BLOCK.values())   # 3416
+C4_PMC_HASH_BLOCKS = 141038165   # SHA-512 blocks of the C4 launch the PMC passes measured (synth is deterministic)
+INT_RATES = [os.path.join(REPO, 'profiles', 'r06_int_rates.json'), os.path.join(REPO, 'profiles', 'r01_int_rates.json')]
+
+
+def _insn_rates(peak):
+    """Measured lane-ops/s of each instruction (tools/ubench/int_rates.hip, the
+    newest committed run), scaled so that its v_mad_u64_u32 equals the best MAD
+    ceiling `peak` (the run's first kernels can start below the sustained clock;
+    scaling up only raises the ceilings the fractions are priced against)."""
+    for path in INT_RATES:
+        try:
+            with open(path) as fh:
+                res = json.load(fh)['results']
+        except (OSError, KeyError, ValueError):
+            continue
+        r = {}
+        for x in res:
+            r[x['insn']] = max(r.get(x['insn'], 0.0), float(x['lane_ops_per_s']))
+        scale = peak / r['v_mad_u64_u32']
+        return {k: v * scale for k, v in r.items()}, os.path.relpath(path, REPO)
+    return None, None
+
+
+def hash_compressions(off):
+    """SHA-512 blocks of SHA-512(R || A || M) over a batch: ceil((64 + len M + 17) / 128)
+    per signature, from the device msg_off."""
+    ln = off[1:] - off[:-1]
+    return int(((ln + 81 + 127) // 128).sum().item())
+
+
+def _hash_roofline(blocks, ms, peak):
+    """k_hash priced like the curve: SHA_INSN_PER_BLOCK lane-instructions per
+    SHA-512 block x the blocks of one launch / its HIP-event duration (pre-checks
+    + k_hash on the launch stream, pv_kernel_timing_sha), against the issue
+    ceiling of that instruction mix at the measured per-instruction rates."""
+    rates, src = _insn_rates(peak)
+    if not rates or ms <= 0:
+        return None
+    miss = [k for k in SHA_W_PER_BLOCK if k not in rates]
+    for k in miss:   # an older rates file: price the missing ones at the half-rate alignbit's rate
+        rates[k] = rates['v_alignbit_b32']
+    t_block = sum(w / rates[k] for k, w in SHA_W_PER_BLOCK.items())   # s per block, whole chip
+    # the C4 k_hash launch's PMC passes (tools/gpu_pmc_r05.sh; k_hash unchanged since):
+    # HBM bytes and executed VALU instructions per SHA-512 block
+    pmc = None
+    try:
+        with open(KEYED_PMC['c4']) as fh:
+            kh = json.load(fh)['kernels']['pv::k_hash']
+        pblocks = C4_PMC_HASH_BLOCKS
+        pmc = {'hbm_bytes_per_block': round(kh['hbm_bytes_per_launch'] / pblocks, 1),
+               'executed_valu_insn_per_block': round(kh['SQ_INSTS_VALU'] * 64 / pblocks, 1),
+               'l2_hit_rate': round(kh['l2_hit_rate'], 3),
+               'source': os.path.relpath(KEYED_PMC['c4'], REPO) + ' (k_hash of the 8M-signature C4 launch, '
+                                                                  '{} blocks)'.format(pblocks)}
+    except (OSError, KeyError, ValueError, TypeError):
+        pass
+    ceiling = 1.0 / t_block
+    rate = blocks / (ms * 1e-3)
+    return {'kernel': 'k_hash (+ k_precheck)', 'blocks': blocks, 'ms': round(ms, 4),
+            'achieved': round(rate * SHA_INSN_PER_BLOCK / 1e12, 3),
+            'peak': round(ceiling * SHA_INSN_PER_BLOCK / 1e12, 3), 'unit': 'T lane-instructions/s',
+            'frac': round(rate / ceiling, 4), 'blocks_per_s': round(rate, 1),
+            'ceiling_blocks_per_s': round(ceiling, 1), 'insn_per_block': dict(SHA_W_PER_BLOCK),
+            'traffic': round(pmc['hbm_bytes_per_block'] * blocks) if pmc else None, 'pmc': pmc,
+            'rates_source': src + (' (no rate for {}: priced at v_alignbit_b32)'.format(miss) if miss else ''),
+            'note': 'W = {} lane-instructions per SHA-512 block (pv_sha512.h, counted per instruction class) x '
+                    'ceil((len M + 81) / 128) blocks per signature from msg_off; time = HIP events from the '
+                    'launch start to the end of k_hash (pre-checks included, k_lattice excluded)'.format(
+                        SHA_INSN_PER_BLOCK)}
+
+
 def _class_rates(peak):
     """Issue rates of the half-rate class (64-bit shifts / adds, v_alignbit,
     v_mul_u32_u24, v_add_co) and of full-rate 32-bit VALU, as ratios to
@@ -811,8 +892,12 @@ def other_configs():
         r['workload'] = (line.get('config') or {}).get('workload')
         rf = line.get('roofline') or {}
         if rf:
-            r['roofline'] = {k: rf.get(k) for k in ('kernel', 'achieved', 'peak', 'unit', 'frac', 'traffic', 'key_prep')
-                             if k != 'key_prep' or rf.get(k)}
+            r['roofline'] = {k: rf.get(k) for k in ('kernel', 'achieved', 'peak', 'unit', 'frac', 'traffic', 'key_prep',
+                                                    'hash', 'stages')
+                             if k not in ('key_prep', 'hash', 'stages') or rf.get(k)}
+            if r['roofline'].get('hash'):
+                r['roofline']['hash'] = {k: r['roofline']['hash'][k] for k in ('ms', 'blocks', 'achieved', 'peak',
+                                                                                'frac')}
         r['child_wall_s'] = round(time.perf_counter() - t0, 2)
         res[name] = r
     return res
@@ -1060,10 +1145,13 @@ def main():
         # launches overlap, so their intervals hold the other stream's work)
         calib = 5
         nat.kernel_timing(local, True)
+        tc0 = time.perf_counter()
         for _ in range(calib):
             batch.verify()
         torch.cuda.synchronize()
+        calib_wall = (time.perf_counter() - tc0) / calib
         calib_sums = nat.kernel_timing(local, False)
+        calib_sha = nat.kernel_timing_sha(local)
     if coll:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1139,8 +1227,13 @@ def main():
     # kernel-level timing for the roofline: HIP events on the launch stream,
     # recorded during the timed steps above (averaged over those launches)
     h_sum, c_sum, launches = nat.kernel_timing(local, False)
+    sha_sum = nat.kernel_timing_sha(local)
+    seq_ms_step = elapsed / args.steps * 1e3
     if pipelined:
         h_sum, c_sum, launches = calib_sums
+        sha_sum = calib_sha
+        seq_ms_step = calib_wall * 1e3
+    ms_sha = sha_sum / max(1, launches)
     ms_hash, ms_curve = h_sum / max(1, launches), c_sum / max(1, launches)
     kernel_ms_on = ('{} sequential calibration steps right before the timed region (pipelined launches overlap)'
                     .format(calib) if pipelined else 'the timed steps')
@@ -1183,6 +1276,18 @@ def main():
     key_prep = None
     if key_cache and not batch.wide:
         key_prep = _key_prep_roofline(batch, args.config, peak)
+    hash_rf = _hash_roofline(hash_compressions(batch.off), ms_sha, peak)
+    # the stages of one sequential step: their HIP-event
+    # durations against the wall time of the sequential steps they were timed on
+    stage_sum = (key_prep['ms'] if key_prep else 0.0) + ms_hash + ms_curve
+    stages = {'key_prep_ms': key_prep['ms'] if key_prep else None, 'sha_ms': round(ms_sha, 4),
+              'lattice_ms': round(ms_hash - ms_sha, 4) if not key_cache else None,
+              'hash_interval_ms': round(ms_hash, 4), 'curve_ms': round(ms_curve, 4),
+              'sum_ms': round(stage_sum, 4), 'sequential_ms_per_step': round(seq_ms_step, 4),
+              'sum_over_sequential': round(stage_sum / seq_ms_step, 4) if seq_ms_step else None,
+              'note': 'HIP-event durations of the priced stages (k_keys after the timed region; hash interval = '
+                      'memset + pre-checks + k_hash (+ k_lattice on generic batches); curve) vs the wall time per '
+                      'step of the {}'.format('5 sequential calibration steps' if pipelined else 'sequential timed steps')}
 
     total = world * n * args.steps
     value = total / elapsed
@@ -1213,6 +1318,8 @@ def main():
                                           'of the step charged to the curve)'},
                      'traffic': traffic,
                      'key_prep': key_prep,
+                     'hash': hash_rf,
+                     'stages': stages,
                      'work_per_verify': wpv,
                      'combined_issue': _combined_issue(n / (ms_curve * 1e-3), peak)
                      if (args.config, n) == ('c2', CONFIGS['c2']['n']) and curve_mode == 'half' else None},

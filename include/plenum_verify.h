@@ -93,7 +93,7 @@ int pv_test_init_dup(uint32_t k);
 
 /* TEST ONLY: the spin budget (ns, default 20,000,000) a zero-copy small call
  * polls its completion word for before it falls back to hipStreamSynchronize;
- * 0 sends every such call through the fallback (tests/test_gpu_latency.py).
+ * 0 sends every such call through the fallback (tests/test_gpu_keycache.py).
  * PV_EINVAL for ns < 0. */
 int pv_test_set_spin_ns(int64_t ns);
 
@@ -399,6 +399,12 @@ int pv_curve_stats(int device, uint32_t *mode, uint64_t *deferred);
  * for the recorded events and returns the summed milliseconds and the number
  * of launches. */
 int pv_kernel_timing(int device, int enable, float *hash_ms, float *curve_ms, uint64_t *launches);
+
+/* The SHA-512 part of the live "hash" interval: summed milliseconds from the
+ * start of each timed verify launch to the end of its k_hash (the pre-checks +
+ * SHA-512(R||A||M), without the half-size path's k_lattice), since the last
+ * pv_kernel_timing(device, 1, ...).  bench.py's hash roofline. */
+int pv_kernel_timing_sha(int device, float *sha_ms);
 
 /* pv_time_verify_device for keyed batches. */
 int pv_time_verify_keyed_device(const uint32_t *ktab, const uint32_t *key_idx, const uint8_t *pk, const uint8_t *sig,

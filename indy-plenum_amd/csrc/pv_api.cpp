@@ -480,12 +480,13 @@ struct Device {
   // pv_kernel_timing: HIP-event times of every verify launch while enabled
   bool live_timing = false;
   float live_hash = 0, live_curve = 0;
+  float live_sha = 0;   // the SHA-512 part of the hash interval (pre-checks + k_hash, no k_lattice)
   uint64_t live_launches = 0;
-  // live timing records three events per launch without waiting (pipelined
+  // live timing records four events per launch without waiting (pipelined
   // callers keep launches in flight); they are resolved when the pool fills
   // up and when timing stops
   struct LiveRec {
-    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};   // start, prep end, curve end, k_hash end
   };
   std::vector<LiveRec> live_pool;
   size_t live_used = 0;
@@ -692,10 +693,12 @@ int resolve_live(Device& d) {
   for (size_t k = 0; k < d.live_used; ++k) {
     hipEvent_t* e = d.live_pool[k].e;
     HIP_OK(hipEventSynchronize(e[2]));
-    float a = 0, b = 0;
+    float a = 0, b = 0, c = 0;
     HIP_OK(hipEventElapsedTime(&a, e[0], e[1]));
     HIP_OK(hipEventElapsedTime(&b, e[1], e[2]));
+    HIP_OK(hipEventElapsedTime(&c, e[0], e[3]));
     d.live_hash += a;
+    d.live_sha += c;
     d.live_curve += b;
   }
   d.live_used = 0;
@@ -726,12 +729,16 @@ bool lat_keyed(const Device& d, const uint32_t* ktab, uint64_t n, bool wide) {
 
 int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                  const uint64_t* off, uint64_t n, uint64_t* bm, hipStream_t s, const uint32_t* ktab,
-                 const uint32_t* kidx, bool wide) {
-  if (lat_keyed(d, ktab, n, wide)) return PV_OK;   // k_verify_quad_keyed runs the whole verify
+                 const uint32_t* kidx, bool wide, hipEvent_t sha_ev = nullptr) {
+  if (lat_keyed(d, ktab, n, wide)) {   // k_verify_quad_keyed runs the whole verify
+    if (sha_ev) HIP_OK(hipEventRecord(sha_ev, s));
+    return PV_OK;
+  }
   if (lat_fused(d, ktab, n)) {
     // k_verify_quad runs the whole verify; only the deferred counter is reset
     HIP_OK(w.qc.ensure(2));
     HIP_OK(hipMemsetAsync(w.qc.p, 0, sizeof(unsigned long long), s));
+    if (sha_ev) HIP_OK(hipEventRecord(sha_ev, s));
     return PV_OK;
   }
   HIP_OK(w.h.ensure(n * 16));
@@ -748,6 +755,8 @@ int enqueue_prep(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig,
   // the half-size path runs the pre-checks in k_lattice (k_hash hashes every
   // signature); keyed and grouped batches in k_precheck before the hash
   HIP_OK(pv::launch_hash(pk, sig, blob, off, n, w.counter.p, w.h.p, half ? nullptr : w.pre.p, d.hash_blocks, s, kidx));
+  // live timing: the SHA-512 stage alone (its roofline in bench.py), before the lattice
+  if (sha_ev) HIP_OK(hipEventRecord(sha_ev, s));
   if (half)
     HIP_OK(pv::launch_lattice(pk, sig, w.h.p, w.pre.p, n, w.hrec.p, w.dlist.p, w.qc.p, w.qc.p + 1, bm,
                               d.mode == CurveMode::Full, s));
@@ -815,7 +824,7 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
   if (rc) return rc;
   if (timed) HIP_OK(hipEventRecord(d.ev[0], s));
   if (lev) HIP_OK(hipEventRecord(lev[0], s));
-  rc = enqueue_prep(d, w, pk, sig, blob, off, n, bm, s, ktab, kidx, wide);
+  rc = enqueue_prep(d, w, pk, sig, blob, off, n, bm, s, ktab, kidx, wide, lev ? lev[3] : nullptr);
   if (rc) return rc;
   // the "hash" interval also holds the scalar stage of the half-size path
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
@@ -1739,13 +1748,25 @@ int pv_kernel_timing(int device, int enable, float* hash_ms, float* curve_ms, ui
     if (rc) return rc;
   }
   if (enable) {
-    d->live_hash = d->live_curve = 0;
+    d->live_hash = d->live_curve = d->live_sha = 0;
     d->live_launches = 0;
   }
   if (hash_ms) *hash_ms = d->live_hash;
   if (curve_ms) *curve_ms = d->live_curve;
   if (launches) *launches = d->live_launches;
   d->live_timing = enable != 0;
+  return PV_OK;
+}
+
+int pv_kernel_timing_sha(int device, float* sha_ms) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  DeviceGuard dg;
+  HIP_OK(hipSetDevice(d->ord));
+  const int rc = resolve_live(*d);
+  if (rc) return rc;
+  if (sha_ms) *sha_ms = d->live_sha;
   return PV_OK;
 }
 

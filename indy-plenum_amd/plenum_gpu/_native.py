@@ -102,6 +102,7 @@ SIGNATURES = [
     ('pv_kernel_timing', ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
       ctypes.POINTER(ctypes.c_uint64)]),
+    ('pv_kernel_timing_sha', ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
 ]
 
 
@@ -112,6 +113,14 @@ def kernel_timing(device, enable):
     _check('pv_kernel_timing', load().pv_kernel_timing(device, 1 if enable else 0, ctypes.byref(h), ctypes.byref(c),
                                                        ctypes.byref(k)))
     return h.value, c.value, k.value
+
+def kernel_timing_sha(device):
+    """Summed ms of the SHA-512 stage (pre-checks + k_hash) of the verify launches
+    timed since kernel_timing(device, True) (pv_kernel_timing_sha)."""
+    v = ctypes.c_float()
+    _check('pv_kernel_timing_sha', load().pv_kernel_timing_sha(device, ctypes.byref(v)))
+    return v.value
+
 
 class Tuning(ctypes.Structure):
     """struct pv_tuning (include/plenum_verify.h): the schedule knobs.  pv_init

@@ -65,6 +65,12 @@ KERNEL(dot2_u32_u16, uint32_t, a + c,
        { asm volatile("v_dot2_u32_u16 %0, %1, %2, %0" : "+v"(acc[c]) : "v"(a), "v"(b)); }, acc[c])
 KERNEL(bfi_b32, uint32_t, a + c,
        { asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(acc[c]) : "v"(a), "v"(b)); }, acc[c])
+KERNEL(bitop3_b32, uint32_t, a + c,
+       { asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(acc[c]) : "v"(a), "v"(b)); }, acc[c])
+KERNEL(lshrrev_b32, uint32_t, a + c,
+       { asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(acc[c])); }, acc[c])
+KERNEL(perm_b32, uint32_t, a + c,
+       { asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(acc[c]) : "v"(a), "v"(0x00010203u)); }, acc[c])
 
 typedef void (*kfn)(uint32_t*, uint32_t);
 
@@ -78,7 +84,11 @@ int main() {
     {"v_add_co_u32", k_add_co_u32}, {"v_lshl_add_u64", k_lshl_add_u64},
     {"v_lshrrev_b64", k_lshrrev_b64}, {"v_fma_f64", k_fma_f64},
     {"v_fma_f32", k_fma_f32}, {"v_dot2_u32_u16", k_dot2_u32_u16},
-    {"v_bfi_b32", k_bfi_b32},
+    {"v_bfi_b32", k_bfi_b32}, {"v_bitop3_b32", k_bitop3_b32}, {"v_lshrrev_b32", k_lshrrev_b32},
+    {"v_perm_b32", k_perm_b32},
+    // the MAD again at the end, after the clock has ramped (the first kernel
+    // of the run can start below the sustained clock)
+    {"v_mad_u64_u32", k_mad_u64_u32},
   };
   int blocks = 256 * 8;
   uint32_t* d;
