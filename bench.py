@@ -129,7 +129,7 @@ def _mad_peak():
 
 TUNED = {}   # pv_tuning fields set from PV_* variables (main)
 CURVE_PMC = os.path.join(REPO, 'profiles', 'r05_curve_pmc.json')   # tools/gpu_final_r05.sh on the round-5 build
-BLS_PMC = os.path.join(REPO, 'profiles', 'r04_bls_pmc.json')
+BLS_PMC = os.path.join(REPO, 'profiles', 'r06_bls_pmc.json')   # tools/gpu_bls_fx6.sh, round-6 build
 # the keyed configs' curve launches (tools/gpu_pmc_r05.sh on the round-5 build)
 KEYED_PMC = {'c3': os.path.join(REPO, 'profiles', 'r05_c3_pmc.json'),
              'c4': os.path.join(REPO, 'profiles', 'r05_c4_pmc.json')}
@@ -672,7 +672,7 @@ def main_bls(args):
                      'traffic': (round(_pmc(BLS_PMC, 'hbm_bytes_per_unit') * n, 1)
                                  if _pmc(BLS_PMC, 'hbm_bytes_per_unit') else None),
                      'traffic_source': 'HBM bytes per check from rocprofv3 FETCH_SIZE / WRITE_SIZE passes '
-                                       '(profiles/r04_bls_pmc.json) x the checks of this launch',
+                                       '(profiles/r06_bls_pmc.json) x the checks of this launch',
                      'note': 'W = {} Fp mul x 180 + {} sqr x 135 v_mad_i64_i32 per check (host op counts of '
                              'the one-lane schedule; the lane pair repeats the inversion of the final '
                              'exponentiation on both lanes, not counted); time = the sigma-prep + pair kernels'

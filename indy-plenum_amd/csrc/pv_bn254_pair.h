@@ -808,9 +808,380 @@ PV_BN_CALL p6 pr_cyc_sqr(pslot<ST> S, const p6& x) {
   return mp_get(S);
 }
 
+// ---- the pair kernel's final exponentiation as a step program (round 6,
+// VERDICT r5 item 2).  Out of line, every Fp12-half product, inverse and
+// Frobenius map of the chain below is a call that saves and restores the
+// callee-saved VGPRs it uses (145 KB of scratch traffic per check,
+// profiles/r04_bls_pmc.json); round 5 inlined them into one loop and the
+// product's working set -- x, y, their swapped halves, t, the three Fp2
+// products, ~360 VGPRs -- spilled (238 KB).  Here the loop holds ONE copy of
+// each operation and the product streams its first operand from the check's
+// LDS slot (both halves: the lane's own for t, both for the Karatsuba sums, so
+// no swapped copy of x is ever held), the second operand's partner half crosses
+// one Fp2 at a time, and the result's sums take the partner's products one Fp2
+// at a time: the product needs y, t and m (~180 VGPRs) instead of ~360.
+// The chain's long-lived values (f, f^u, f^u^2, t0, t1) are parked in a private
+// array (FX_SLOTS halves).  A step: acc = post(op(pre_a(X_a), pre_b(X_b))), X =
+// acc (FX_ACC) or a parked slot, pre = the Frobenius map n (bits 0-1) then a
+// conjugation (bit 2); op FX_MUL the product, FX_INV the inverse of X_a, FX_CYC n
+// cyclotomic squarings of X_a in the LDS slot (n in the b field, a reduction
+// after every fourth: pr_pow_u's schedule); post = conjugation; then acc may be
+// parked.  The operands and their order are final_exp's (the chain below), and
+// every product forms pr_mul's sums, so every value has the same limbs.
+// PV_FE_PROG = 0 builds the chain of calls (A/B).
+#ifndef PV_FE_PROG
+#define PV_FE_PROG 1
+#endif
+#ifndef PV_FX_YHOLD
+#define PV_FX_YHOLD 0   // 1: the three Y = y + y' held through the m products (A/B)
+#endif
+constexpr uint32_t FX_MUL = 0, FX_INV = 1, FX_CYC = 2;
+constexpr uint32_t FX_ACC = 7, FX_NONE = 15;
+constexpr int FX_SLOTS = 5;   // 0 f (f0 before step 2), 1 f^u, 2 f^u^2, 3 t0, 4 t1
+constexpr uint32_t FX_CONJ = 4, FX_F1 = 1, FX_F2 = 2, FX_F3 = 3;
+constexpr uint32_t fx(uint32_t op, uint32_t a, uint32_t pa, uint32_t b, uint32_t pb, uint32_t post, uint32_t park) {
+  return op | a << 4 | pa << 8 | b << 12 | pb << 20 | post << 24 | park << 28;
+}
+constexpr uint32_t fx_mul(uint32_t a, uint32_t pa, uint32_t b, uint32_t pb, uint32_t post = 0,
+                          uint32_t park = FX_NONE) {
+  return fx(FX_MUL, a, pa, b, pb, post, park);
+}
+constexpr uint32_t fx_cyc(uint32_t a, uint32_t n, uint32_t park = FX_NONE) { return fx(FX_CYC, a, 0, n, 0, 0, park); }
+constexpr int FX_STEPS = 32;
+constexpr uint32_t FX_PROG[FX_STEPS] = {
+    fx(FX_INV, FX_ACC, 0, 0, 0, 0, FX_NONE),              //  0 1 / f0
+    fx_mul(0, FX_CONJ, FX_ACC, 0),                        //  1 conj(f0) / f0
+    fx_mul(FX_ACC, FX_F2, FX_ACC, 0, 0, 0),               //  2 f = frob2(f) f
+    fx_cyc(FX_ACC, 7), fx_mul(FX_ACC, 0, 0, 0),           //  3, 4 pow_u(f)
+    fx_cyc(FX_ACC, 55), fx_mul(FX_ACC, 0, 0, 0, 1, 1),    //  5, 6 -> fu
+    fx_cyc(FX_ACC, 7), fx_mul(FX_ACC, 0, 1, 0),           //  7, 8 pow_u(fu)
+    fx_cyc(FX_ACC, 55), fx_mul(FX_ACC, 0, 1, 0, 1, 2),    //  9, 10 -> fu2
+    fx_cyc(FX_ACC, 7), fx_mul(FX_ACC, 0, 2, 0),           // 11, 12 pow_u(fu2)
+    fx_cyc(FX_ACC, 55), fx_mul(FX_ACC, 0, 2, 0, 1),       // 13, 14 -> fu3
+    fx_mul(FX_ACC, 0, FX_ACC, FX_F1, 1),                  // 15 y6 = conj(fu3 frob1(fu3))
+    fx_cyc(FX_ACC, 1, 3),                                 // 16 t0 = cyc_sqr(y6)
+    fx_mul(1, 0, 2, FX_F1, 1),                            // 17 conj(fu frob1(fu2))
+    fx_mul(3, 0, FX_ACC, 0),                              // 18 t0 = t0 (17)
+    fx_mul(FX_ACC, 0, 2, FX_CONJ, 0, 3),                  // 19 t0 = t0 y5, y5 = conj(fu2)
+    fx_mul(1, FX_F1 | FX_CONJ, 2, FX_CONJ),               // 20 conj(frob1(fu)) y5
+    fx_mul(FX_ACC, 0, 3, 0, 0, 4),                        // 21 t1 = (20) t0
+    fx_mul(3, 0, 2, FX_F2, 0, 3),                         // 22 t0 = t0 frob2(fu2)
+    fx_cyc(4, 1), fx_mul(FX_ACC, 0, 3, 0),                // 23, 24 t1 = cyc_sqr(t1) t0
+    fx_cyc(FX_ACC, 1, 4),                                 // 25 t1 = cyc_sqr(t1)
+    fx_mul(FX_ACC, 0, 0, FX_CONJ, 0, 3),                  // 26 t0 = t1 conj(f)
+    fx_mul(0, FX_F1, 0, FX_F2),                           // 27 frob1(f) frob2(f)
+    fx_mul(FX_ACC, 0, 0, FX_F3),                          // 28 y0 = (27) frob3(f)
+    fx_mul(4, 0, FX_ACC, 0, 0, 4),                        // 29 t1 = t1 y0
+    fx_cyc(3, 1), fx_mul(FX_ACC, 0, 4, 0),                // 30, 31 cyc_sqr(t0) t1
+};
+static_assert(FX_PROG[FX_STEPS - 1] == fx_mul(FX_ACC, 0, 4, 0), "program length");
+
+// limbwise role select (v_cndmask per limb): a select of whole structs can be
+// lowered to a select of their addresses, which puts both in scratch
+PV_HD fp2 f2pick(bool h, const fp2& x, const fp2& y) {
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    r.a.l[i] = h ? x.a.l[i] : y.a.l[i];
+    r.b.l[i] = h ? x.b.l[i] : y.b.l[i];
+  }
+  return r;
+}
+
+// coefficient k of a lane's Fp6 half (k a compile-time constant after unrolling)
+PV_HD const fp2& f6c(const fp6& x, int k) { return k == 0 ? x.c0 : (k == 1 ? x.c1 : x.c2); }
+PV_HD p2 p6c(const p6& x, int k) {
+  p2 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) r.e[j] = f6c(x.e[j], k);
+  return r;
+}
+
+// gamma_{n,e} (the Frobenius map n's constant of the coefficient of w^e, e =
+// 2k + role; e = 0: the Montgomery one) as (a, b) limb pointers, so that the
+// pre-map runs with k a runtime (wave-uniform) value: one copy of the map
+PV_BN_CONST uint32_t FX_ZERO[NL] = {};
+PV_BN_CONST const uint32_t* FX_GP[3][6][2] = {
+    {{ONE_M, FX_ZERO}, {G1_1_A, G1_1_B}, {G1_2_A, G1_2_B}, {G1_3_A, G1_3_B}, {G1_4_A, G1_4_B}, {G1_5_A, G1_5_B}},
+    {{ONE_M, FX_ZERO}, {G2_1_A, FX_ZERO}, {G2_2_A, FX_ZERO}, {G2_3_A, FX_ZERO}, {G2_4_A, FX_ZERO}, {G2_5_A, FX_ZERO}},
+    {{ONE_M, FX_ZERO}, {G3_1_A, G3_1_B}, {G3_2_A, G3_2_B}, {G3_3_A, G3_3_B}, {G3_4_A, G3_4_B}, {G3_5_A, G3_5_B}},
+};
+// coefficient k of the Frobenius map n (0..3) of a lane's half, then a
+// conjugation (bit 2): pr_frob2 / pr_frob_odd / pr_conj one coefficient at a
+// time (the same multiplies by the same constants, so the same limbs)
+PV_HD p2 fx_pre_c(const p2& x, int k, uint32_t pre) {
+  const uint32_t n = pre & 3u;
+  p2 r = x;
+  if (n != 0) {
+    const uint32_t* const* g0 = FX_GP[n - 1][2 * k];       // role 0: w^(2k)
+    const uint32_t* const* g1 = FX_GP[n - 1][2 * k + 1];   // role 1: w^(2k+1)
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int h = prole(j);
+      if (n == 2) {
+        const fp c0 = cst(g0[0]), c1 = cst(g1[0]);
+        fp g;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) g.l[i] = h ? c1.l[i] : c0.l[i];
+        r.e[j] = f2mulfp(x.e[j], g);
+      } else {
+        r.e[j] = f2mul(f2conj(x.e[j]), f2pick(h, fp2{cst(g1[0]), cst(g1[1])}, fp2{cst(g0[0]), cst(g0[1])}));
+      }
+    }
+  }
+  if (pre & FX_CONJ) {
+#pragma unroll
+    for (int j = 0; j < PL; ++j) r.e[j] = f2pick(prole(j), f2neg(r.e[j]), r.e[j]);
+  }
+  return r;
+}
+PV_HD int fx_slot(uint32_t a) { return a < (uint32_t)FX_SLOTS ? (int)a : 0; }
+// The parked halves: fx_park[3 * slot + k] holds coefficient k of each lane's
+// half (PL of them on the host).  The slot index is wave-uniform (it comes from
+// FX_PROG): made scalar, every access is a scalar base + constant offset, and no
+// per-slot copy of the operand code is generated.
+PV_HD uint32_t fx_uni(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_readfirstlane(x);
+#else
+  return x;
+#endif
+}
+PV_HD p2 fx_park_c(const p2 (&park)[3 * FX_SLOTS], uint32_t x, int k) { return park[3 * fx_uni(fx_slot(x)) + k]; }
+PV_HD void fx_park_st(p2 (&park)[3 * FX_SLOTS], uint32_t x, const p6& v) {
+  const uint32_t u = fx_uni(x);
+  if (u >= (uint32_t)FX_SLOTS) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) park[3 * u + k] = p6c(v, k);
+}
+
+
+// x y with x (both halves) in the slot S and y the lanes' halves in registers:
+// pr_mul's products and sums.  Role 0 forms t0 = x.a y.a, role 1 t1 = x.b y.b
+// (f6mul_i's products on the lane's own half of x, read from the slot when each
+// product starts, folded into three lazy sums as f6mul_fold does); the third
+// product's Fp2 products m (role 0 X_k Y_k, role 1 the Karatsuba sums) from X =
+// x.a + x.b (both halves from the slot) and Y = y + y' (the partner's half of y
+// crossing one Fp2 at a time).  Then pr_mul_tail's sums, with the partner's m
+// and t crossing one Fp2 at a time.
+template <int ST>
+PV_HD void pr_mul_s(pslot<ST> S, const p6& y, bool conj) {
+  p2 m[3];
+  {
+#if PV_FX_YHOLD
+    p2 Y[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const p2 yk = p6c(y, k), yo = pswap(yk);
+#pragma unroll
+      for (int j = 0; j < PL; ++j) Y[k].e[j] = f2add(yk.e[j], yo.e[j]);
+    }
+    mp_fence();
+    auto Yk = [&](int k, int j) -> fp2 { return Y[k].e[j]; };
+#else
+    // Y_k = y_k + y'_k formed where each product needs it (the partner's Fp2
+    // crossing again): no three Y's held through the m products
+    auto Yk = [&](int k, int j) -> fp2 {
+      const p2 yk = p6c(y, k), yo = pswap(yk);
+      return f2add(yk.e[j], yo.e[j]);
+    };
+#endif
+    // (a, b) of role 1's Karatsuba factor of m_k; role 0 takes X_k Y_k
+    constexpr int KA[3] = {1, 0, 0}, KB[3] = {2, 1, 2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int j = 0; j < PL; ++j) {
+        const int h = prole(j);
+        const fp2 Xa = f2add(S.ld(KA[k]), S.ld(3 + KA[k])), Xb = f2add(S.ld(KB[k]), S.ld(3 + KB[k]));
+        const fp2 Xk = f2add(S.ld(k), S.ld(3 + k));
+        m[k].e[j] = pin(f2mul(f2pick(h, f2addL(Xa, Xb), Xk), f2pick(h, f2add(Yk(KA[k], j), Yk(KB[k], j)), Yk(k, j))));
+      }
+      mp_fence();
+    }
+  }
+  p6 t;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int X = 3 * prole(j);
+    const fp6& b = y.e[j];
+    fp2 c0, c1, c2;
+    {
+      const fp2 v0 = pin(f2mul(S.ld(X), b.c0));
+      c0 = v0;
+      c1 = f2negL(v0);
+      c2 = f2negL(v0);
+    }
+    mp_fence();
+    {
+      const fp2 v1 = pin(f2mul(S.ld(X + 1), b.c1));
+      c0 = f2subL(c0, f2mulxiL(v1));
+      c1 = f2subL(c1, v1);
+      c2 = f2addL(c2, v1);
+    }
+    mp_fence();
+    {
+      const fp2 v2 = pin(f2mul(S.ld(X + 2), b.c2));
+      const fp2 xv2 = f2mulxiL(v2);
+      c0 = f2subL(c0, xv2);
+      c1 = f2addL(c1, xv2);
+      c2 = f2subL(c2, v2);
+    }
+    mp_fence();
+    c0 = f2addL(c0, f2mulxiL(pin(f2mul(f2addL(S.ld(X + 1), S.ld(X + 2)), f2add(b.c1, b.c2)))));
+    mp_fence();
+    c1 = f2addL(c1, pin(f2mul(f2addL(S.ld(X), S.ld(X + 1)), f2add(b.c0, b.c1))));
+    mp_fence();
+    c2 = f2addL(c2, pin(f2mul(f2addL(S.ld(X), S.ld(X + 2)), f2add(b.c0, b.c2))));
+    t.e[j] = fp6{f2norm(c0), f2norm(c1), f2norm(c2)};
+  }
+  mp_fence();
+  // pr_mul_tail: role 0 writes t0 + v t1, role 1 s - t0 - t1 (s from the m's)
+  p2 sc[3];
+  {
+    const p2 mo[3] = {pswap(m[0]), pswap(m[1]), pswap(m[2])};
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const fp2 &v0 = mo[0].e[j], &v1 = mo[1].e[j], &v2 = mo[2].e[j];
+      const fp2 &s12 = m[0].e[j], &s01 = m[1].e[j], &s02 = m[2].e[j];
+      sc[0].e[j] = f2norm(f2addL(f2mulxiL(f2subL(f2subL(s12, v1), v2)), v0));
+      sc[1].e[j] = f2norm(f2addL(f2subL(f2subL(s01, v0), v1), f2mulxiL(v2)));
+      sc[2].e[j] = f2norm(f2addL(f2subL(f2subL(s02, v0), v2), v1));
+    }
+  }
+  // every read of x is done: the result overwrites it, each lane its own half
+  mp_fence();
+  // role 0: ra_k = t0_k + (xi t1_2 | t1_0 | t1_1); role 1: rb_k = sc_k - t0_k - t1_k
+  constexpr int RT[3] = {2, 0, 1};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const p2 tk = p6c(t, k), tko = pswap(tk);
+    const p2 tr = p6c(t, RT[k]), tro = pswap(tr);
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int h = prole(j);
+      // (value selects: a select of references puts both operands in memory)
+      const fp2 t0k = f2pick(h, tko.e[j], tk.e[j]);
+      const fp2 t1k = f2pick(h, tk.e[j], tko.e[j]);
+      const fp2 rb = f2norm(f2subL(f2subL(sc[k].e[j], t0k), t1k));
+      const fp2 t1r = tro.e[j];   // role 0's partner (role 1) t1 at RT[k]
+      const fp2 ra = f2norm(f2addL(tk.e[j], k == 0 ? f2mulxiL(t1r) : t1r));
+      fp2 v = f2pick(h, rb, ra);
+      if (conj) v = f2pick(h, f2neg(v), v);   // pr_conj: role 1's half negated
+      S.st(3 * h + k, v);
+    }
+  }
+  mp_fence();
+}
+
+// 1 / x with both Fp6 products inlined (the step program's one copy)
+PV_HD p6 pr_inv_i(const p6& x) {
+  p6 sq;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) sq.e[j] = f6mul_fold(x.e[j], x.e[j]);
+  const p6 so = pswap(sq);
+  p6 r;
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    const int h = prole(j);
+    const fp6 d = f6inv(f6sub(f6sel(h, so.e[j], sq.e[j]), f6mulv(f6sel(h, sq.e[j], so.e[j]))));
+    const fp6 m = f6mul_fold(x.e[j], d);
+    r.e[j] = f6sel(h, f6neg(m), m);
+  }
+  return r;
+}
+
+// The accumulator lives in the check's LDS slot (each lane its own half), never
+// in registers across steps.  Operand X into the slot with its pre-map, one Fp2
+// at a time: a parked half copied in, or acc mapped in place.
+template <int ST>
+PV_HD void fx_put(pslot<ST> S, const p2 (&park)[3 * FX_SLOTS], uint32_t x, uint32_t pre) {
+  if (x == FX_ACC && pre == 0) return;
+#pragma unroll 1
+  for (int k = 0; k < 3; ++k) {
+    p2 c;
+    if (x == FX_ACC) {
+#pragma unroll
+      for (int j = 0; j < PL; ++j) c.e[j] = S.ld(3 * prole(j) + k);
+    } else {
+      c = fx_park_c(park, x, k);
+    }
+    c = fx_pre_c(c, k, pre);
+#pragma unroll
+    for (int j = 0; j < PL; ++j) S.st(3 * prole(j) + k, c.e[j]);
+    mp_fence();
+  }
+}
+
+// operand X with its pre-map in registers (acc read from the slot)
+template <int ST>
+PV_HD p6 fx_get(pslot<ST> S, const p2 (&park)[3 * FX_SLOTS], uint32_t x, uint32_t pre) {
+  p6 r;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    p2 c;
+    if (x == FX_ACC) {
+#pragma unroll
+      for (int j = 0; j < PL; ++j) c.e[j] = S.ld(3 * prole(j) + k);
+    } else {
+      c = fx_park_c(park, x, k);
+    }
+    c = fx_pre_c(c, k, pre);
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      if (k == 0) r.e[j].c0 = c.e[j];
+      else if (k == 1) r.e[j].c1 = c.e[j];
+      else r.e[j].c2 = c.e[j];
+    }
+  }
+  mp_fence();
+  return r;
+}
+
+// final_exp(f0) on halves as FX_PROG: one loop, one copy of each operation.
+// Inlined into the pair kernel (one call site): as a call it saved and restored
+// the callee-saved VGPRs it uses on every check.
+#ifndef PV_FX_CALL
+#define PV_FX_CALL PV_HD
+#endif
+template <int ST>
+PV_FX_CALL p6 pr_final_exp_fx(pslot<ST> S, const p6& f0) {
+  p2 park[3 * FX_SLOTS];
+  fx_park_st(park, 0, f0);
+  mp_put(S, f0);
+#pragma unroll 1
+  for (int s = 0; s < FX_STEPS; ++s) {
+    const uint32_t w = FX_PROG[s];
+    const uint32_t op = w & 15u, a = (w >> 4) & 15u, b = (w >> 12) & 255u;
+    const bool post = (w >> 24) & 1u;
+    if (op == FX_MUL) {
+      // B first: it may be the accumulator the slot is about to receive A over
+      const p6 B = fx_get(S, park, b, (w >> 20) & 15u);
+      fx_put(S, park, a, (w >> 8) & 15u);
+      pr_mul_s(S, B, post);
+    } else {
+      if (op == FX_INV) {
+        static_assert(FX_PROG[0] == fx(FX_INV, FX_ACC, 0, 0, 0, 0, FX_NONE), "the inverse takes acc, unmapped");
+        mp_put(S, pr_inv_i(mp_get(S)));
+      } else {
+        fx_put(S, park, a, (w >> 8) & 15u);
+#pragma unroll 1
+        for (uint32_t i = 0; i < b; ++i) {
+          mp_cyc_sqr(S);
+          if ((i & 3) == 3) mp_reduce(S);
+        }
+      }
+      if (post) mp_put(S, pr_conj(mp_get(S)));
+    }
+    const uint32_t pk = w >> 28;
+    if (pk < (uint32_t)FX_SLOTS) fx_park_st(park, pk, mp_get(S));   // (pk: an SGPR; uniform branch)
+  }
+  return mp_get(S);
+}
+
 // final_exp's chain on halves
 template <int ST, int LV = 0>
-PV_BN_CALL p6 pr_final_exp(pslot<ST> S, const p6& f0) {
+PV_BN_CALL p6 pr_final_exp_chain(pslot<ST> S, const p6& f0) {
   p6 f = pmul<LV>(pr_conj(f0), pinv<LV>(f0));   // ^(p^6 - 1)
   f = pmul<LV>(pr_frob2(f), f);              // ^(p^2 + 1)
   const p6 fu = pr_pow_u<ST, LV>(S, f);
@@ -829,6 +1200,12 @@ PV_BN_CALL p6 pr_final_exp(pslot<ST> S, const p6& f0) {
   const p6 y0 = pmul<LV>(pmul<LV>(pr_frob1(f), pr_frob2(f)), pr_frob3(f));
   t1 = pmul<LV>(t1, y0);
   return pmul<LV>(pr_cyc_sqr<ST, LV>(S, t0), t1);
+}
+// the pair kernel (LV 0) runs the step program, the quad / octet the chain
+template <int ST, int LV = 0>
+PV_HD p6 pr_final_exp(pslot<ST> S, const p6& f0) {
+  if constexpr (LV == 0 && PV_FE_PROG) return pr_final_exp_fx<ST>(S, f0);
+  return pr_final_exp_chain<ST, LV>(S, f0);
 }
 
 #if defined(__HIPCC__)

@@ -7,7 +7,7 @@ set -u
 out=${1:-gpurun_out/closing5}
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-bash tools/gpu_r05_suite.sh "$out/suite" && \
+bash tools/gpu_suite.sh "$out/suite" && \
 echo "[closing] $(date +%T) bench" && \
 timeout -k 10 600 python bench.py > "$out/bench.json" 2> "$out/bench.err" && \
 echo "[closing] $(date +%T) stats" && \

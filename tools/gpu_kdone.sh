@@ -8,7 +8,7 @@ set -u
 out=${1:-gpurun_out/kdone}
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-bash tools/gpu_r05_suite.sh "$out/suite" && \
+bash tools/gpu_suite.sh "$out/suite" && \
 for r in 1 2 3; do
   for lib in indy-plenum_amd/lib/libplenum_verify.so indy-plenum_amd/lib/ab/signal_launch.so; do
     tag=$(basename $lib .so)

@@ -11,6 +11,6 @@ for lib in indy-plenum_amd/lib/libplenum_verify.so indy-plenum_amd/lib/ab/kflag_
   tag=$(basename $lib .so)
   PLENUM_GPU_LIB=$lib PV_LAT_CACHED=1 PV_LAT_SIZES=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/$tag" -o run -- python3 tools/latency.py > "$out/$tag.log" 2>&1 || exit 1
 done && \
-bash tools/gpu_r05_suite.sh "$out/suite" && \
+bash tools/gpu_suite.sh "$out/suite" && \
 PV_LAT_CACHED=1 PV_LAT_SIZES=1,16,100,1000,4096 timeout -k 10 200 python3 tools/latency.py > "$out/lat_cached.jsonl" 2>/dev/null && \
 PV_LAT_SIZES=1,16,100,1000,4096 timeout -k 10 200 python3 tools/latency.py > "$out/lat_uncached.jsonl" 2>/dev/null && echo done

@@ -8,7 +8,7 @@ out=${1:-gpurun_out/latab}; var=$2
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 main=indy-plenum_amd/lib/libplenum_verify.so
-bash tools/gpu_r05_suite.sh "$out/suite" && \
+bash tools/gpu_suite.sh "$out/suite" && \
 for lib in $main $var; do
   tag=$(basename $lib .so)
   PLENUM_GPU_LIB=$lib PV_LAT_CACHED=1 PV_LAT_SIZES=1,100 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof_$tag" -o run -- python3 tools/latency.py > "$out/prof_$tag.log" 2>&1 || exit 1

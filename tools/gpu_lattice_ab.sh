@@ -8,7 +8,7 @@ out=${1:-gpurun_out/latab}; var=$2
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 main=indy-plenum_amd/lib/libplenum_verify.so
-bash tools/gpu_r05_suite.sh "$out/suite" && \
+bash tools/gpu_suite.sh "$out/suite" && \
 for lib in $main $var; do
   tag=$(basename $lib .so)
   PLENUM_GPU_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/seq_$tag" -o run -- python3 bench.py --steps 10 --warmup 3 \

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The -m gpu suite and smoke() on the current build (log per step under OUT).
-#   bash tools/gpu_r05_suite.sh OUT
+#   bash tools/gpu_suite.sh OUT
 set -u
 out=${1:-gpurun_out/suite}
 mkdir -p "$out"

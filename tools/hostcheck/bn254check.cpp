@@ -184,6 +184,40 @@ int bnc_verify_quad(const uint8_t* sig128, const uint8_t* m, uint64_t n, const u
   return one ? 1 : 0;
 }
 
+// the pair kernel's final exponentiation as a step program (pr_final_exp_fx, the
+// product streaming x from the slot) against the chain of calls (the same
+// template at level 1, which on the host runs the pair operations), limb by
+// limb, on the quad schedule's Miller product of this check: 1 = identical
+int bnc_fe_prog_vs_chain(const uint8_t* sig128, const uint8_t* m, uint64_t n, const uint8_t* pk128,
+                         const uint8_t* gen128) {
+  static uint32_t gl[N_LINES * LINE_WORDS], pl[N_LINES * LINE_WORDS];
+  if (bnc_g2_lines(gen128, gl) != 0) return -1;
+  g2a q;
+  if (g2_decode(pk128, q) != 0) return -1;
+  g2_lines(pl, q);
+  uint8_t h[128];
+  bnc_hash_to_g1(m, n, h);
+  const fp hx = to_mont(from_be32(h + 1)), hy = to_mont(from_be32(h + 33));
+  fp xqh, yqh, xs, ys, xq = fzero(), yq = fzero();
+  line_point(hx, hy, true, xqh, yqh);
+  bool s_inf;
+  g1_decode(sig128, xs, ys, s_inf);
+  if (s_inf) return -1;
+  line_point(xs, ys, false, xq, yq);
+  p1 qa[2], qb[2];
+  for (int j = 0; j < PL; ++j) {
+    qa[0].e[j] = qa[1].e[j] = fsel(prole(j), yq, xq);
+    qb[0].e[j] = qb[1].e[j] = fsel(prole(j), yqh, xqh);
+  }
+  uint32_t sa[12 * NL], sb[12 * NL];
+  const p6 fa = miller_pair<1, true>(pslot<1>{sa}, gl, nullptr, qa);
+  const p6 fb = miller_pair<1, true>(pslot<1>{sb}, pl, nullptr, qb);
+  const p6 f = pr_mul(fa, fb);
+  const p6 r0 = pr_final_exp<1, 0>(pslot<1>{sa}, f);
+  const p6 r1 = pr_final_exp<1, 1>(pslot<1>{sb}, f);
+  return memcmp(&r0, &r1, sizeof r0) == 0 ? 1 : 0;
+}
+
 // the Fp multiplies / squarings of ONE check as k_bls_verify runs it (sigma
 // decoding + bls_check; the lines and H(m) are per key / per message and are
 // prepared before the counters are reset): out = {mul, sqr}
