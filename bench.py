@@ -157,6 +157,16 @@ def _key_prep_roofline(batch, config, peak, reps=3):
     b.record()
     b.synchronize()
     ms = a.elapsed_time(b) / reps
+    if batch.wide:
+        # k_keys_wide (C3's node keys): 128 lanes per key redo the decode and the
+        # chain to A_q (latency over work), so its MAD fraction is not a kernel
+        # efficiency; W = the host-counted work of the 128 slices of one key
+        wk = W_MUL_KEYPREP_WIDE * 100 + W_SQ_KEYPREP_WIDE * 55
+        return {'kernel': 'k_keys_wide', 'keys': k, 'ms': round(ms, 4),
+                'achieved': round(wk * k / (ms * 1e-3) / 1e12, 3), 'peak': round(peak / 1e12, 3),
+                'frac': round(wk * k / (ms * 1e-3) / peak, 4), 'traffic': None,
+                'note': 'W = {} v_mad lane-ops per key over its 128 table slices (host op count) / HIP-event '
+                        'duration, {} launches after the timed region'.format(int(wk), reps)}
     work = (W_MUL_KEYPREP * 100 + W_SQ_KEYPREP * 55) * k
     traffic = _pmc(KEYED_PMC[config], 'key_prep_hbm_bytes_per_launch') if config == 'c4' else None
     return {'kernel': 'k_keys', 'keys': k, 'ms': round(ms, 4), 'achieved': round(work / (ms * 1e-3) / 1e12, 3),
@@ -1274,7 +1284,7 @@ def main():
     achieved_step = work / (ms_step * 1e-3)
     peak = _mad_peak()
     key_prep = None
-    if key_cache and not batch.wide:
+    if key_cache:
         key_prep = _key_prep_roofline(batch, args.config, peak)
     hash_rf = _hash_roofline(hash_compressions(batch.off), ms_sha, peak)
     # the stages of one sequential step: their HIP-event
