@@ -875,6 +875,14 @@ constexpr uint32_t FX_PROG[FX_STEPS] = {
     fx_cyc(3, 1), fx_mul(FX_ACC, 0, 4, 0),                // 30, 31 cyc_sqr(t0) t1
 };
 static_assert(FX_PROG[FX_STEPS - 1] == fx_mul(FX_ACC, 0, 4, 0), "program length");
+#if defined(__HIPCC__)
+// the device copy the kernel reads with a lane-indexed vector load
+__device__ const uint32_t FX_PROG_DEV[FX_STEPS] = {
+    FX_PROG[0], FX_PROG[1], FX_PROG[2], FX_PROG[3], FX_PROG[4], FX_PROG[5], FX_PROG[6], FX_PROG[7],
+    FX_PROG[8], FX_PROG[9], FX_PROG[10], FX_PROG[11], FX_PROG[12], FX_PROG[13], FX_PROG[14], FX_PROG[15],
+    FX_PROG[16], FX_PROG[17], FX_PROG[18], FX_PROG[19], FX_PROG[20], FX_PROG[21], FX_PROG[22], FX_PROG[23],
+    FX_PROG[24], FX_PROG[25], FX_PROG[26], FX_PROG[27], FX_PROG[28], FX_PROG[29], FX_PROG[30], FX_PROG[31]};
+#endif
 
 // limbwise role select (v_cndmask per limb): a select of whole structs can be
 // lowered to a select of their addresses, which puts both in scratch
@@ -898,35 +906,48 @@ PV_HD p2 p6c(const p6& x, int k) {
 }
 
 // gamma_{n,e} (the Frobenius map n's constant of the coefficient of w^e, e =
-// 2k + role; e = 0: the Montgomery one) as (a, b) limb pointers, so that the
-// pre-map runs with k a runtime (wave-uniform) value: one copy of the map
+// 2k + role; e = 0: the Montgomery one) as (a, b) limb pointers.  Indexed with
+// compile-time k only (the callers unroll k), so every constant is an immediate:
+// the check kernels read no data through the scalar cache beyond their kernel
+// arguments (tests/test_isa_guards.py), and n, a wave-uniform runtime value,
+// selects between immediates, never between addresses.
 PV_BN_CONST uint32_t FX_ZERO[NL] = {};
 PV_BN_CONST const uint32_t* FX_GP[3][6][2] = {
     {{ONE_M, FX_ZERO}, {G1_1_A, G1_1_B}, {G1_2_A, G1_2_B}, {G1_3_A, G1_3_B}, {G1_4_A, G1_4_B}, {G1_5_A, G1_5_B}},
     {{ONE_M, FX_ZERO}, {G2_1_A, FX_ZERO}, {G2_2_A, FX_ZERO}, {G2_3_A, FX_ZERO}, {G2_4_A, FX_ZERO}, {G2_5_A, FX_ZERO}},
     {{ONE_M, FX_ZERO}, {G3_1_A, G3_1_B}, {G3_2_A, G3_2_B}, {G3_3_A, G3_3_B}, {G3_4_A, G3_4_B}, {G3_5_A, G3_5_B}},
 };
+PV_HD fp fx_cst_sel(bool c, const uint32_t* x, const uint32_t* y) {   // c ? x : y, limbwise
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = (int32_t)(c ? x[i] : y[i]);
+  return r;
+}
 // coefficient k of the Frobenius map n (0..3) of a lane's half, then a
 // conjugation (bit 2): pr_frob2 / pr_frob_odd / pr_conj one coefficient at a
 // time (the same multiplies by the same constants, so the same limbs)
-PV_HD p2 fx_pre_c(const p2& x, int k, uint32_t pre) {
+template <int K>
+PV_HD p2 fx_pre_c(const p2& x, uint32_t pre) {
   const uint32_t n = pre & 3u;
   p2 r = x;
-  if (n != 0) {
-    const uint32_t* const* g0 = FX_GP[n - 1][2 * k];       // role 0: w^(2k)
-    const uint32_t* const* g1 = FX_GP[n - 1][2 * k + 1];   // role 1: w^(2k+1)
+  if (n == 2) {
 #pragma unroll
     for (int j = 0; j < PL; ++j) {
-      const int h = prole(j);
-      if (n == 2) {
-        const fp c0 = cst(g0[0]), c1 = cst(g1[0]);
-        fp g;
+      const fp g = fx_cst_sel(prole(j), FX_GP[1][2 * K + 1][0], FX_GP[1][2 * K][0]);
+      r.e[j] = f2mulfp(x.e[j], g);
+    }
+  } else if (n != 0) {
+    const bool one = n == 1;
 #pragma unroll
-        for (int i = 0; i < NL; ++i) g.l[i] = h ? c1.l[i] : c0.l[i];
-        r.e[j] = f2mulfp(x.e[j], g);
-      } else {
-        r.e[j] = f2mul(f2conj(x.e[j]), f2pick(h, fp2{cst(g1[0]), cst(g1[1])}, fp2{cst(g0[0]), cst(g0[1])}));
-      }
+    for (int j = 0; j < PL; ++j) {
+      const int e = 2 * K + prole(j);
+      // (e is role-dependent: both roles' constants as immediates, then selects)
+      const fp2 g1{fx_cst_sel(one, FX_GP[0][2 * K + 1][0], FX_GP[2][2 * K + 1][0]),
+                   fx_cst_sel(one, FX_GP[0][2 * K + 1][1], FX_GP[2][2 * K + 1][1])};
+      const fp2 g0{fx_cst_sel(one, FX_GP[0][2 * K][0], FX_GP[2][2 * K][0]),
+                   fx_cst_sel(one, FX_GP[0][2 * K][1], FX_GP[2][2 * K][1])};
+      (void)e;
+      r.e[j] = f2mul(f2conj(x.e[j]), f2pick(prole(j), g1, g0));
     }
   }
   if (pre & FX_CONJ) {
@@ -1094,46 +1115,46 @@ PV_HD p6 pr_inv_i(const p6& x) {
 // The accumulator lives in the check's LDS slot (each lane its own half), never
 // in registers across steps.  Operand X into the slot with its pre-map, one Fp2
 // at a time: a parked half copied in, or acc mapped in place.
+template <int ST, int K>
+PV_HD void fx_put_c(pslot<ST> S, const p2 (&park)[3 * FX_SLOTS], uint32_t x, uint32_t pre) {
+  p2 c;
+  if (x == FX_ACC) {
+#pragma unroll
+    for (int j = 0; j < PL; ++j) c.e[j] = S.ld(3 * prole(j) + K);
+  } else {
+    c = fx_park_c(park, x, K);
+  }
+  c = fx_pre_c<K>(c, pre);
+#pragma unroll
+  for (int j = 0; j < PL; ++j) S.st(3 * prole(j) + K, c.e[j]);
+  mp_fence();
+}
 template <int ST>
 PV_HD void fx_put(pslot<ST> S, const p2 (&park)[3 * FX_SLOTS], uint32_t x, uint32_t pre) {
   if (x == FX_ACC && pre == 0) return;
-#pragma unroll 1
-  for (int k = 0; k < 3; ++k) {
-    p2 c;
-    if (x == FX_ACC) {
-#pragma unroll
-      for (int j = 0; j < PL; ++j) c.e[j] = S.ld(3 * prole(j) + k);
-    } else {
-      c = fx_park_c(park, x, k);
-    }
-    c = fx_pre_c(c, k, pre);
-#pragma unroll
-    for (int j = 0; j < PL; ++j) S.st(3 * prole(j) + k, c.e[j]);
-    mp_fence();
-  }
+  fx_put_c<ST, 0>(S, park, x, pre);
+  fx_put_c<ST, 1>(S, park, x, pre);
+  fx_put_c<ST, 2>(S, park, x, pre);
 }
-
 // operand X with its pre-map in registers (acc read from the slot)
+template <int ST, int K>
+PV_HD p2 fx_get_c(pslot<ST> S, const p2 (&park)[3 * FX_SLOTS], uint32_t x, uint32_t pre) {
+  p2 c;
+  if (x == FX_ACC) {
+#pragma unroll
+    for (int j = 0; j < PL; ++j) c.e[j] = S.ld(3 * prole(j) + K);
+  } else {
+    c = fx_park_c(park, x, K);
+  }
+  return fx_pre_c<K>(c, pre);
+}
 template <int ST>
 PV_HD p6 fx_get(pslot<ST> S, const p2 (&park)[3 * FX_SLOTS], uint32_t x, uint32_t pre) {
+  const p2 c0 = fx_get_c<ST, 0>(S, park, x, pre), c1 = fx_get_c<ST, 1>(S, park, x, pre),
+           c2 = fx_get_c<ST, 2>(S, park, x, pre);
   p6 r;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    p2 c;
-    if (x == FX_ACC) {
-#pragma unroll
-      for (int j = 0; j < PL; ++j) c.e[j] = S.ld(3 * prole(j) + k);
-    } else {
-      c = fx_park_c(park, x, k);
-    }
-    c = fx_pre_c(c, k, pre);
-#pragma unroll
-    for (int j = 0; j < PL; ++j) {
-      if (k == 0) r.e[j].c0 = c.e[j];
-      else if (k == 1) r.e[j].c1 = c.e[j];
-      else r.e[j].c2 = c.e[j];
-    }
-  }
+  for (int j = 0; j < PL; ++j) r.e[j] = fp6{c0.e[j], c1.e[j], c2.e[j]};
   mp_fence();
   return r;
 }
@@ -1149,9 +1170,20 @@ PV_FX_CALL p6 pr_final_exp_fx(pslot<ST> S, const p6& f0) {
   p2 park[3 * FX_SLOTS];
   fx_park_st(park, 0, f0);
   mp_put(S, f0);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the program's words, word s in lane s of one VGPR (a lane-indexed vector
+  // load), read back with v_readlane: no scalar-cache load of the table
+  static_assert(FX_STEPS <= 64, "one word per lane");
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t progv = FX_PROG_DEV[lane < (uint32_t)FX_STEPS ? lane : 0u];
+#endif
 #pragma unroll 1
   for (int s = 0; s < FX_STEPS; ++s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)progv, s);
+#else
     const uint32_t w = FX_PROG[s];
+#endif
     const uint32_t op = w & 15u, a = (w >> 4) & 15u, b = (w >> 12) & 255u;
     const bool post = (w >> 24) & 1u;
     if (op == FX_MUL) {
