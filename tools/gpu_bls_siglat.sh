@@ -3,6 +3,8 @@
 # exponentiation instead of a root then an inversion).  BLS GPU tests, then
 # lone-check / 3PC-batch latencies interleaved against -D PV_SIGPREP_PAIR=0
 # (indy-plenum_amd/lib/ab_sigprep_one.so), three rounds, and a kernel trace.
+# Not adopted: the variant is tools/ab/bls_sigprep_pair_notadopted.patch (apply it
+# and add the PV_SIGPREP_PAIR switch to rebuild the A/B pair).
 #   bash tools/gpu_bls_siglat.sh OUT
 set -u
 out=${1:-gpurun_out/siglat}
