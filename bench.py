@@ -225,6 +225,15 @@ SHA_W_PER_BLOCK = {'v_alignbit_b32': 80 * 12 + 64 * 10, 'v_bitop3_b32': 80 * 8 +
 SHA_INSN_PER_BLOCK = sum(SHA_W_PER_BLOCK.values())   # 3416
 C4_PMC_HASH_BLOCKS = 141038165   # SHA-512 blocks of the C4 launch the PMC passes measured (synth is deterministic)
 INT_RATES = [os.path.join(REPO, 'profiles', 'r06_int_rates.json'), os.path.join(REPO, 'profiles', 'r01_int_rates.json')]
+# k_sha256 (row f3): one SHA-256 compression per 64-byte block, pv_sha256.h's
+# native 32-bit form: 64 rounds x (Sigma0, Sigma1: 3 v_alignbit_b32 each; their
+# xors, Ch, Maj: 1 v_bitop3_b32 each; K + W, the three-way t1 sum as v_add3_u32 +
+# v_add_u32, t2, e, a) + 48 schedule words x (sigma0, sigma1: 2 alignbit + 1
+# v_lshrrev_b32 + 1 bitop3 each; the four-way sum as v_add3_u32 + v_add_u32) + 8
+# state adds + the big-endian decode of 16 words (v_perm_b32)
+SHA256_W_PER_BLOCK = {'v_alignbit_b32': 64 * 6 + 48 * 4, 'v_bitop3_b32': 64 * 4 + 48 * 2, 'v_lshrrev_b32': 48 * 2,
+                      'v_add3_u32': 64 + 48, 'v_add_u32': 64 * 5 + 48 + 8, 'v_perm_b32': 16}
+SHA256_INSN_PER_BLOCK = sum(SHA256_W_PER_BLOCK.values())   # 1528
 
 
 def _insn_rates(peak):
@@ -292,6 +301,32 @@ def _hash_roofline(blocks, ms, peak):
                     'ceil((len M + 81) / 128) blocks per signature from msg_off; time = HIP events from the '
                     'launch start to the end of k_hash (pre-checks included, k_lattice excluded)'.format(
                         SHA_INSN_PER_BLOCK)}
+
+
+def _sha256_roofline(blocks, ms, peak, step_blocks=None, step_ms=None):
+    """k_sha256 priced per SHA-256 block like k_hash: SHA256_INSN_PER_BLOCK
+    lane-instructions x the blocks of one launch / its duration, against that
+    instruction mix at the measured per-instruction rates."""
+    rates, src = _insn_rates(peak)
+    if not rates or ms <= 0:
+        return None
+    t_block = sum(w / rates[k] for k, w in SHA256_W_PER_BLOCK.items())
+    ceiling = 1.0 / t_block
+    rate = blocks / (ms * 1e-3)
+    out = {'bound': 'valu', 'kernel': 'k_sha256 (leaf digests, prefix 0x00)', 'blocks': blocks, 'ms': round(ms, 4),
+           'achieved': round(rate * SHA256_INSN_PER_BLOCK / 1e12, 3),
+           'peak': round(ceiling * SHA256_INSN_PER_BLOCK / 1e12, 3), 'unit': 'T lane-instructions/s',
+           'frac': round(rate / ceiling, 4), 'traffic': None, 'insn_per_block': dict(SHA256_W_PER_BLOCK),
+           'rates_source': src,
+           'note': 'W = {} lane-instructions per SHA-256 block (pv_sha256.h, per instruction class) x ceil((1 + 256 + '
+                   '9) / 64) = 5 blocks per leaf; time = HIP events around pv_sha256_batch_device on the launch '
+                   'stream, after the timed region'.format(SHA256_INSN_PER_BLOCK)}
+    if step_blocks and step_ms:
+        out['per_step'] = {'blocks': step_blocks, 'ms': round(step_ms, 4),
+                           'frac': round(step_blocks / (step_ms * 1e-3) / ceiling, 4),
+                           'note': 'every block of the step (5 per leaf + 2 per internal node) / the step time: '
+                                   'the 20 level launches charged too'}
+    return out
 
 
 def _class_rates(peak):
@@ -759,6 +794,20 @@ def main_f3(args):
         step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # the leaf kernel alone, for its roofline: pv_sha256_batch_device over the same
+    # leaves (k_sha256, prefix 0x00), HIP events on the launch stream
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    nat._check('pv_sha256_batch_device', lib.pv_sha256_batch_device(_p(blob), _p(off), n, 0, _p(leaves), 0,
+                                                                    _stream(dev)))
+    ev0.record()
+    for _ in range(5):
+        nat._check('pv_sha256_batch_device', lib.pv_sha256_batch_device(_p(blob), _p(off), n, 0, _p(leaves), 0,
+                                                                        _stream(dev)))
+    ev1.record()
+    ev1.synchronize()
+    leaf_ms = ev0.elapsed_time(ev1) / 5
+    leaf_blocks = n * ((1 + ln + 9 + 63) // 64)
+    step_blocks = leaf_blocks + (n - 1) * ((1 + 64 + 9 + 63) // 64)
     # check: root of the same leaves with hashlib (level-wise RFC 6962)
     host = blob[:n * ln].cpu().numpy()
     lvl = [hashlib.sha256(b'\x00' + host[i * ln:(i + 1) * ln].tobytes()).digest() for i in range(n)]
@@ -860,7 +909,7 @@ def main_f3(args):
         'sha256_batch_small': {'rows': small, 'dispatch_items': 512,
                                'path': 'sha256_batch(host list of 256 B leaves, prefix 0x00): hashlib vs one GPU '
                                        'call incl. pack + H2D + D2H, mean of 5'},
-        'roofline': None,
+        'roofline': _sha256_roofline(leaf_blocks, leaf_ms, _mad_peak(), step_blocks, elapsed / args.steps * 1e3),
         'cpu_baseline': {'value': round(cpu_rate, 1), 'unit': 'leaves/s', 'cores': 1, 'kind': 'port',
                          'sample': 'hashlib SHA-256 tree hash (the reference TreeHasher algorithm, level-wise) over '
                                    'the first {} leaves on 1 host thread'.format(sample)},
