@@ -1239,6 +1239,11 @@ hipError_t launch_tally_bits(const uint32_t* bits, const uint32_t* dup, uint64_t
 }
 
 // ----------------------------------------------- SHA-256 / Merkle (row f3)
+// PV_SHA256_PREFETCH = 1: each lane's next block window is loaded during the
+// current compression (one trip ahead) instead of right before it
+#ifndef PV_SHA256_PREFETCH
+#define PV_SHA256_PREFETCH 1
+#endif
 // Batch SHA-256 of (prefix || M_i): persistent lanes with per-lane refill, the
 // same work-queue scheme as k_hash (ragged messages cost no divergence;
 // wave-private index chunks, next message's offsets loaded one message ahead).
@@ -1254,6 +1259,10 @@ __global__ __launch_bounds__(256) void k_sha256(const uint8_t* __restrict__ blob
     nme = off[nidx + 1];
   }
   uint32_t hs[8];
+#if PV_SHA256_PREFETCH
+  uint32_t y[17];   // the window of the block this lane compresses next
+  if (nidx < n) sha256_window(y, blob + nmo, nme - nmo, plen, 0);
+#endif
   while (true) {
     const bool promote = blk == nblk && nidx < n;
     if (promote) {
@@ -1276,7 +1285,15 @@ __global__ __launch_bounds__(256) void k_sha256(const uint8_t* __restrict__ blob
     if (!__any(active)) break;   // every message promotes on the trip it is taken
     if (active) {
       uint32_t w[16];
+#if PV_SHA256_PREFETCH
+      sha256_assemble(w, y, blob + mo, ml, plen, prefix, blk, nblk);
+      // the next trip's window in flight during this compression: block blk + 1,
+      // or block 0 of the queued message (whose offsets are already loaded)
+      if (blk + 1 < nblk) sha256_window(y, blob + mo, ml, plen, blk + 1);
+      else if (nidx < n) sha256_window(y, blob + nmo, nme - nmo, plen, 0);
+#else
       sha256_block(w, blob + mo, ml, plen, prefix, blk, nblk);
+#endif
       sha256_compress(hs, w);
       if (++blk == nblk) {
         uint32_t* o = out + 8 * idx;

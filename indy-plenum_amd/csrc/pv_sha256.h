@@ -93,17 +93,26 @@ PV_HD uint64_t sha256_blocks(uint64_t mlen, uint32_t plen) { return (plen + mlen
 // block `blk` of (prefix || M) as 16 big-endian words, SHA padding and length
 // applied.  Guarded aligned loads: the blob needs >= 16 readable bytes after the
 // last message.
-PV_HD void sha256_block(uint32_t w[16], const uint8_t* m, uint64_t mlen, uint32_t plen, uint32_t prefix, uint64_t blk,
-                        uint64_t nblk) {
+// the aligned-word window of block blk of (prefix || M): 17 words from the
+// aligned-down first data byte, zero past the message (no load issued there)
+PV_HD void sha256_window(uint32_t y[17], const uint8_t* m, uint64_t mlen, uint32_t plen, uint64_t blk) {
   const bool pre = plen != 0 && blk == 0;
   const uint64_t q = pre ? 0 : 64 * blk - plen;        // first data byte of the window
   const int64_t rem = (int64_t)mlen - (int64_t)q;
   const uintptr_t base = reinterpret_cast<uintptr_t>(m) + q;
   const uint32_t mis = (uint32_t)(base & 3u);
   const uint32_t* wp = reinterpret_cast<const uint32_t*>(base - mis);
-  uint32_t y[17], d[16];
 #pragma unroll
   for (int k = 0; k < 17; ++k) y[k] = (int64_t)(4 * k) - (int64_t)mis < rem ? wp[k] : 0u;
+}
+// block blk's 16 big-endian words from its window: funnel shift by the
+// misalignment, the prefix byte, the 0x80 terminator and the bit length
+PV_HD void sha256_assemble(uint32_t w[16], const uint32_t y[17], const uint8_t* m, uint64_t mlen, uint32_t plen,
+                           uint32_t prefix, uint64_t blk, uint64_t nblk) {
+  const bool pre = plen != 0 && blk == 0;
+  const uint64_t q = pre ? 0 : 64 * blk - plen;
+  const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + q) & 3u);
+  uint32_t d[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) d[k] = funnel32_(y[k + 1], y[k], 8u * mis);
   if (pre) {  // shift the data one byte up and put the prefix in byte 0
@@ -127,6 +136,12 @@ PV_HD void sha256_block(uint32_t w[16], const uint8_t* m, uint64_t mlen, uint32_
     w[14] = (uint32_t)(bits >> 32);
     w[15] = (uint32_t)bits;
   }
+}
+PV_HD void sha256_block(uint32_t w[16], const uint8_t* m, uint64_t mlen, uint32_t plen, uint32_t prefix, uint64_t blk,
+                        uint64_t nblk) {
+  uint32_t y[17];
+  sha256_window(y, m, mlen, plen, blk);
+  sha256_assemble(w, y, m, mlen, plen, prefix, blk, nblk);
 }
 
 // digest of (prefix || M) as 8 little-endian words (digest byte order)
