@@ -135,6 +135,11 @@ __device__ __forceinline__ uint64_t wave_task(unsigned long long* tasks) {
 #ifndef PV_HASH_LDS
 #define PV_HASH_LDS 0
 #endif
+// 16-byte groups of the next block's message window loaded one compression
+// ahead (0 = none)
+#ifndef PV_HASH_PF
+#define PV_HASH_PF 0
+#endif
 // libsodium's pre-checks on (R, S, A), one
 // lane per signature, ahead of the hash: keeps the branchy, load-dependent
 // check out of k_hash's refill path (which every ragged C4 iteration hit).
@@ -176,6 +181,11 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
     }
   };
   prefetch();
+#if PV_HASH_PF
+  // first groups of the next block's window (tagged by message offset + block)
+  uint32_t ypf[4 * PV_HASH_PF];
+  uint64_t pf_mo = ~0ull, pf_blk = 0;
+#endif
 #if PV_HASH_LDS
   // Message blocks are staged through LDS by the whole wavefront: lane l's
   // 144-byte window (9 groups of 16 B) is cut into 9 parts and part p is
@@ -265,8 +275,32 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
     if (active) {
 #if !PV_HASH_LDS
       uint32_t y[MSG_Y];
+#if PV_HASH_PF
+      // the window's first PV_HASH_PF groups were loaded during the previous
+      // compression when the tag matches; the rest now
+      if (pf_mo == mo && pf_blk == blk) {
+#pragma unroll
+        for (int k = 0; k < 4 * PV_HASH_PF; ++k) y[k] = ypf[k];
+        msg_fetch_part(y + 4 * PV_HASH_PF, blob + mo, ml, hram_q(blk), blk == 0, PV_HASH_PF, 9);
+      } else {
+        msg_fetch(y, blob + mo, ml, hram_q(blk), blk == 0);
+      }
+#else
       msg_fetch(y, blob + mo, ml, hram_q(blk), blk == 0);
+#endif
       hram_assemble_ra(w, y, ra, blob + mo, ml, blk, nblk);
+#if PV_HASH_PF
+      // next trip's block: blk + 1 of this message, or block 0 of the queued one
+      if (blk + 1 < nblk) {
+        pf_mo = mo;
+        pf_blk = blk + 1;
+        msg_fetch_part(ypf, blob + mo, ml, hram_q(blk + 1), false, 0, PV_HASH_PF);
+      } else if (nidx < n) {
+        pf_mo = nmo;
+        pf_blk = 0;
+        msg_fetch_part(ypf, blob + nmo, nme - nmo, 0, true, 0, PV_HASH_PF);
+      }
+#endif
 #endif
       sha512_compress(hs, w);
       if (++blk == nblk) {

@@ -174,6 +174,32 @@ PV_HD uint32_t bitsel(uint32_t m, uint32_t a, uint32_t b) {
 #endif
 }
 
+#ifndef PV_FETCH_WORDS
+// groups [g0, g1) of msg_fetch's window only (the same guards): k_hash loads
+// the window's first groups one compression ahead (PV_HASH_PF)
+PV_HD void msg_fetch_part(uint32_t* y, const uint8_t* m, uint64_t mlen, uint64_t q, bool first, int g0, int g1) {
+  const int64_t rem = (int64_t)mlen - (int64_t)q;
+  const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + q) & 3u);
+  const uint32_t* wp = reinterpret_cast<const uint32_t*>(m + q - mis);
+#pragma unroll
+  for (int g = 0; g < 9; ++g) {
+    if (g < g0 || g >= g1) continue;
+    const bool ld = (int64_t)(16 * g) - (int64_t)mis < rem && (!first || g < 5);
+    uint32_t a = 0, b = 0, c = 0, d = 0;
+    if (ld) {
+      a = wp[4 * g];
+      b = wp[4 * g + 1];
+      c = wp[4 * g + 2];
+      d = wp[4 * g + 3];
+    }
+    y[4 * (g - g0)] = a;
+    y[4 * (g - g0) + 1] = b;
+    y[4 * (g - g0) + 2] = c;
+    y[4 * (g - g0) + 3] = d;
+  }
+}
+#endif
+
 PV_HD void msg_assemble(uint32_t x[32], const uint32_t y[MSG_Y], const uint8_t* m, uint64_t mlen, uint64_t q) {
   const int64_t rem64 = (int64_t)mlen - (int64_t)q;
   // rem clamped to [-1, 132] (every word full above 128, all zero below 0)
