@@ -1070,6 +1070,9 @@ def main():
                     help='prepared-key format: auto = wide (radix-256 comb) for node keys (c3), narrow for key pools')
     ap.add_argument('--no-key-cache', action='store_true',
                     help='c3/c4: re-decompress every key per signature instead of preparing each distinct key once')
+    ap.add_argument('--keys-serial', action='store_true',
+                    help='c3/c4 pipelined: prepare the keys before the hash stage on the step\'s stream (default: on '
+                         'the slot\'s side stream, beside the hash stage; pv_verify_keys_device_async)')
     ap.add_argument('--collective', action='store_true',
                     help='create the process group and run the verdict / quorum all-gathers even at one rank '
                          '(RCCL exercised on a one-GPU box; the gathered bytes are checked like at N > 1)')
@@ -1191,7 +1194,7 @@ def main():
         slot = counter[0] & 1
         counter[0] += 1
         with torch.cuda.stream(streams[slot]):
-            verdict, bitmap = batch.verify_async(slot, streams[slot])
+            verdict, bitmap = batch.verify_async(slot, streams[slot], keys_beside=not args.keys_serial)
             finish(slot, verdict, bitmap)
 
     for _ in range(args.warmup):
@@ -1388,6 +1391,12 @@ def main():
                     if pipelined else 'sequential: one stream',
         'cpu_baseline': None,
     }
+    if key_cache and pipelined:
+        out['key_schedule'] = ('serial: key preparation before the hash stage on the step\'s stream'
+                               if args.keys_serial else
+                               'pv_verify_keys_device_async: key preparation on the slot\'s side stream while the '
+                               'hash stage runs when the key grid is under one wave per SIMD (C3\'s node keys), '
+                               'else before it on the step\'s stream (C4\'s key pool)')
     if tally is not None:
         out['config']['batches_per_gpu'] = tally['nb']
         out['config']['quorum'] = tally['q']

@@ -196,6 +196,22 @@ int pv_verify_keyed_wide_device_async(const uint32_t *ktab, const uint32_t *key_
                                       const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n,
                                       uint8_t *verdict, uint64_t *bitmap, int device, void *stream, int slot);
 
+/* Key preparation + keyed verification of one batch in one enqueue-only call
+ * (slot / stream rules as pv_*_device_async): the k keys in pk are prepared
+ * into ktab (wide = 0: the PV_KEY_WORDS format, 1: PV_KEY_WORDS_WIDE).  A key
+ * grid of less than one wave per SIMD (e.g. a pool's 25 node keys in the wide
+ * format) runs on the slot's own side stream, forked from `stream`, WHILE the
+ * signatures' SHA-512 stage runs on `stream` (it reads only the key bytes
+ * pk[key_idx[i]]), and the keyed curve kernel waits for both; a larger key
+ * grid fills the GPU itself and runs before the hash stage on `stream`.  Same
+ * verdicts and tables as
+ * pv_keys_prepare[_wide]_device_async followed by
+ * pv_verify_keyed[_wide]_device_async on the same stream, which run the two
+ * stages one after the other.  n = 0 only prepares the keys. */
+int pv_verify_keys_device_async(const uint8_t *pk, uint64_t k, uint32_t *ktab, const uint32_t *key_idx,
+                                const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n,
+                                uint8_t *verdict, uint64_t *bitmap, uint32_t wide, int device, void *stream, int slot);
+
 /* SHA-256 / Merkle tree hashing.
  *   pv_sha256_batch[_device]  digests[i] (32 bytes) = SHA-256(prefix || M_i); prefix -1 = none,
  *                             0..255 = that single byte.  Replaces the per-request

@@ -450,6 +450,11 @@ struct Device {
   PinBuf vout;  // page-locked verdicts of the shard (D2H target; copied to the caller after the drain)
   hipEvent_t staged[2] = {nullptr, nullptr};  // slot i's H2D has finished
   hipEvent_t keys_ready = nullptr;            // prepared-key table built (host pipeline, ws[0] -> ws[1])
+  // pv_verify_keys_device_async: slot i's key preparation runs on kside[i],
+  // forked from the caller's stream after the workspace's previous use (kfork)
+  // and joined back before the curve kernel (kjoin), so it overlaps the hash stage
+  hipStream_t kside[2] = {nullptr, nullptr};
+  hipEvent_t kfork[2] = {nullptr, nullptr}, kjoin[2] = {nullptr, nullptr};
   int cu_count = 0;
   int curve_blocks = 0;
   int hash_blocks = 0;
@@ -595,6 +600,11 @@ int init_device(Device& d) {
   HIP_OK(hipEventCreateWithFlags(&d.keys_ready, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&d.joined, hipEventDisableTiming));
   for (auto& w : d.ws) HIP_OK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+  for (int i = 0; i < 2; ++i) {
+    HIP_OK(hipStreamCreateWithFlags(&d.kside[i], hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&d.kfork[i], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&d.kjoin[i], hipEventDisableTiming));
+  }
   d.zc_in.flags = d.zc_out.flags = d.zc_flag.flags = hipHostMallocCoherent | hipHostMallocMapped;
   apply_tuning(d, g_tune);
   hipDeviceProp_t prop;
@@ -646,6 +656,13 @@ void release_device(Device& d) {
   (void)hipSetDevice(d.ord);
   for (auto& w : d.ws)
     if (w.stream) (void)hipStreamSynchronize(w.stream);
+  for (int i = 0; i < 2; ++i) {
+    if (d.kside[i]) (void)hipStreamSynchronize(d.kside[i]), (void)hipStreamDestroy(d.kside[i]);
+    if (d.kfork[i]) (void)hipEventDestroy(d.kfork[i]);
+    if (d.kjoin[i]) (void)hipEventDestroy(d.kjoin[i]);
+    d.kside[i] = nullptr;
+    d.kfork[i] = d.kjoin[i] = nullptr;
+  }
   d.btab.release(); d.bw.release(); d.counter.release();
   for (auto& w : d.ws) w.release();
   if (d.ws[1].stream) (void)hipStreamDestroy(d.ws[1].stream);
@@ -802,7 +819,7 @@ int enqueue_curve(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig
 int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* sig, const uint8_t* blob,
                    const uint64_t* off, uint64_t n, uint8_t* verdict, uint64_t* bitmap, hipStream_t s, bool timed,
                    float* ms_hash, float* ms_curve, const uint32_t* ktab = nullptr, const uint32_t* kidx = nullptr,
-                   bool wide = false) {
+                   bool wide = false, hipEvent_t curve_after = nullptr) {
   if (n == 0) return PV_OK;
   const bool live = !timed && d.live_timing;
   hipEvent_t* lev = nullptr;
@@ -829,6 +846,9 @@ int enqueue_verify(Device& d, Workspace& w, const uint8_t* pk, const uint8_t* si
   // the "hash" interval also holds the scalar stage of the half-size path
   if (timed) HIP_OK(hipEventRecord(d.ev[1], s));
   if (lev) HIP_OK(hipEventRecord(lev[1], s));
+  // keys prepared on a side stream (pv_verify_keys_device_async): the curve
+  // kernel reads their tables
+  if (curve_after) HIP_OK(hipStreamWaitEvent(s, curve_after, 0));
   rc = enqueue_curve(d, w, pk, sig, blob, off, n, verdict, bm, s, ktab, kidx, wide);
   if (rc) return rc;
   rc = ws_end(w, s);
@@ -1694,6 +1714,57 @@ int pv_verify_keyed_wide_device_async(const uint32_t* ktab, const uint32_t* key_
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
   return enqueue_verify(*d, d->ws[slot], pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr,
                         ktab, key_idx, true);
+}
+
+// key preparation beside the hash stage: the keys are built on the slot's side
+// stream while k_hash runs on `s`; the keyed curve waits for both
+int pv_verify_keys_device_async(const uint8_t* pk, uint64_t k, uint32_t* ktab, const uint32_t* key_idx,
+                                const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off, uint64_t n,
+                                uint8_t* verdict, uint64_t* bitmap, uint32_t wide, int device, void* stream, int slot) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceGuard dg;
+  Device* d = find_dev(device);
+  if (!d) return fail(PV_ENOTINIT, "device %d not initialised (call pv_init)", device);
+  if (slot < 0 || slot > 1) return fail(PV_EINVAL, "slot must be 0 or 1");
+  if (wide > 1) return fail(PV_EINVAL, "wide must be 0 or 1");
+  if (k == 0 && n == 0) return PV_OK;
+  if (n > 0 && k == 0) return fail(PV_EINVAL, "signatures without keys");
+  if (!pk || !ktab || (n > 0 && (!key_idx || !sig || !msg_blob || !msg_off || !verdict || !bitmap)))
+    return fail(PV_EINVAL, "null device buffer");
+  HIP_OK(hipSetDevice(d->ord));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d->ws[slot].stream;
+  Workspace& w = d->ws[slot];
+  // the slot's key table and key scratch were last used by its previous batch:
+  // fork after that (ws_begin orders s), join before the curve
+  int rc = ws_begin(w, s);
+  if (rc) return rc;
+  // beside the hash stage only when the key grid is small (less than one wave
+  // per SIMD: C3's 25 wide node keys, a latency-bound 50-wave grid): a key
+  // grid that fills the GPU (C4's 2^20 keys) competes with k_hash for the
+  // same issue slots and ran 1.3 % slower beside it
+  // (profiles/r06_ab_keys_beside.jsonl), so it stays in line on `s`
+  const uint64_t lanes = wide ? k * (uint64_t)pv::KEYTAB_WIDE_LANES : k;
+  const bool side = lanes <= 64ull * 4 * (uint64_t)d->cu_count;
+  hipStream_t ks = side ? d->kside[slot] : s;
+  if (side) {
+    HIP_OK(hipEventRecord(d->kfork[slot], s));
+    HIP_OK(hipStreamWaitEvent(ks, d->kfork[slot], 0));
+  }
+  DevBuf<uint32_t>& scr = slot ? d->kscr2 : d->kscr;
+  if (wide) {
+    HIP_OK(scr.ensure(k * pv::KEYTAB_WIDE_LANES * (uint64_t)pv::KEYTAB_WIDE_SCRATCH));
+    HIP_OK(pv::launch_keys_wide(pk, k, ktab, scr.p, ks));
+  } else {
+    HIP_OK(scr.ensure((k + 63) / 64 * 64 * pv::KEYTAB_SCRATCH));
+    HIP_OK(pv::launch_keys(pk, k, ktab, scr.p, ks));
+  }
+  if (side) HIP_OK(hipEventRecord(d->kjoin[slot], ks));
+  if (n == 0) {
+    if (side) HIP_OK(hipStreamWaitEvent(s, d->kjoin[slot], 0));
+    return ws_end(w, s);
+  }
+  return enqueue_verify(*d, w, pk, sig, msg_blob, msg_off, n, verdict, bitmap, s, false, nullptr, nullptr, ktab, key_idx,
+                        wide != 0, side ? d->kjoin[slot] : nullptr);
 }
 
 int pv_time_verify_keyed_device(const uint32_t* ktab, const uint32_t* key_idx, const uint8_t* pk, const uint8_t* sig,

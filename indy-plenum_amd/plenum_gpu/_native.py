@@ -62,6 +62,9 @@ SIGNATURES = [
      [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp]),
     ('pv_verify_keyed_wide_device_async', ctypes.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, _vp, ctypes.c_int]),
+    ('pv_verify_keys_device_async', ctypes.c_int,
+     [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_int, _vp,
+      ctypes.c_int]),
     ('pv_sha256_batch', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int32, _vp]),
     ('pv_sha256_batch_device', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int32, _vp, ctypes.c_int, _vp]),
     ('pv_merkle_root', ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),

@@ -129,15 +129,24 @@ class SyntheticBatch:
                          (torch.empty_like(self.verdict), torch.zeros_like(self.bitmap),
                           None if self.ktab is None else torch.empty_like(self.ktab))]
 
-    def verify_async(self, slot, stream):
+    def verify_async(self, slot, stream, keys_beside=True):
         """Enqueue one pass of the hot path on `stream` with workspace/output
         `slot` (pv_*_async): returns (verdict, bitmap) of the slot without
-        waiting.  Two passes in flight must use different slots."""
+        waiting.  Two passes in flight must use different slots.  With the key
+        cache, keys_beside prepares the keys on the slot's side stream while the
+        hash stage runs (pv_verify_keys_device_async); False runs the two
+        stages one after the other on `stream`."""
         lib = nat.load()
         verdict, bitmap, ktab = self.slot_out[slot]
         s = ctypes.c_void_p(stream.cuda_stream)
         dev = self.device.index
-        if self.keys is not None:
+        if self.keys is not None and keys_beside:
+            upk, kidx = self.keys
+            nat._check('pv_verify_keys_device_async',
+                       lib.pv_verify_keys_device_async(_p(upk), upk.shape[0], _p(ktab), _p(kidx), _p(self.sig),
+                                                       _p(self.blob), _p(self.off), self.n, _p(verdict), _p(bitmap),
+                                                       int(self.wide), dev, s, slot))
+        elif self.keys is not None:
             upk, kidx = self.keys
             w = '_wide' if self.wide else ''
             fp, fv = 'pv_keys_prepare{}_device_async'.format(w), 'pv_verify_keyed{}_device_async'.format(w)

@@ -267,20 +267,33 @@ def test_c4_full_shard(torch_dev):
     assert not want.all() and want.any()
 
 
-@pytest.mark.parametrize('keyed', [False, True])
-def test_pipelined_async_slots(torch_dev, keyed):
+@pytest.mark.parametrize('keyed,beside', [(False, True), (True, True), (True, False), ('wide', True)])
+def test_pipelined_async_slots(torch_dev, keyed, beside):
     """bench.py's pipelined schedule: passes alternate over two streams with
     verify workspaces / output sets 0 and 1 (pv_*_device_async), several in
     flight at once; every slot's verdicts and bitmap equal the synchronous
-    pass, and the generic path matches the oracle on a sample."""
+    pass, and the generic path matches the oracle on a sample.  Keyed passes
+    either prepare the keys on the slot's side stream beside the hash stage
+    (pv_verify_keys_device_async, `beside`) or before it on the same stream;
+    either way every slot's key table equals the synchronous preparation's."""
     torch = torch_dev
+    from plenum_gpu import synth
     from plenum_gpu.device import SyntheticBatch
     n = 200_000
-    b = SyntheticBatch(0, n, 128, cfg=4, mode=1, mlen_max=1024, key_mod=4096 if keyed else 0)
-    b.use_key_cache(keyed)
+    if keyed == 'wide':   # C3's shape: 25 node keys in the radix-256 format
+        b = SyntheticBatch(0, 25 * 8000, 0, cfg=3, first=25 * 31, mode=synth.COMMIT, n_nodes=25)
+        b.use_key_cache(True, wide=True)
+        n = b.n
+    else:
+        b = SyntheticBatch(0, n, 128, cfg=4, mode=1, mlen_max=1024, key_mod=4096 if keyed else 0)
+        b.use_key_cache(keyed)
     b.make_slots()
+    if keyed:   # padding words of the tables are never written: the same fill in both slots
+        for slot in range(2):
+            b.slot_out[slot][2].fill_(-1)
     want = b.verify().cpu().numpy().copy()
     want_bits = b.bitmap.cpu().numpy().copy()
+    want_tab = b.ktab.cpu().numpy().copy() if keyed else None
     tamper = b.tamper.cpu().numpy().astype(bool)
     assert (want.astype(bool) == ~tamper).all()
     for slot in range(2):
@@ -290,12 +303,14 @@ def test_pipelined_async_slots(torch_dev, keyed):
     streams = [torch.cuda.Stream(b.device), torch.cuda.Stream(b.device)]
     for k in range(6):
         with torch.cuda.stream(streams[k & 1]):
-            b.verify_async(k & 1, streams[k & 1])
+            b.verify_async(k & 1, streams[k & 1], keys_beside=beside)
     torch.cuda.synchronize()
     for slot in range(2):
-        v, bm, _ = b.slot_out[slot]
+        v, bm, kt = b.slot_out[slot]
         assert (v.cpu().numpy() == want).all()
         assert (bm.cpu().numpy() == want_bits).all()
+        if keyed:
+            assert (kt.cpu().numpy() == want_tab).all()
     if not keyed:
         idx = np.random.default_rng(1).choice(n, 200, replace=False)
         off = b.off.cpu().numpy().astype(np.uint64)
