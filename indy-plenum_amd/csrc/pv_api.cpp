@@ -2043,6 +2043,10 @@ int pv_sign_batch(const uint8_t* seeds, const uint8_t* msg_blob, const uint64_t*
 
 namespace {
 // leaf digests (n x 8 words) -> root (8 words) on stream s, all device memory
+// PV_MERKLE_TAIL_ON = 0: one k_merkle_level launch per level down to the root (A/B)
+#ifndef PV_MERKLE_TAIL_ON
+#define PV_MERKLE_TAIL_ON 1
+#endif
 int enqueue_merkle(Device& d, const uint8_t* blob, const uint64_t* off, uint64_t n, uint32_t* leaves, uint32_t* root,
                    hipStream_t s) {
   if (n == 0) {  // hash_empty(): SHA-256 of the empty string (ledger/tree_hasher.py:17-19)
@@ -2056,6 +2060,10 @@ int enqueue_merkle(Device& d, const uint8_t* blob, const uint64_t* off, uint64_t
   uint64_t m = n;
   int which = 0;
   while (m > 1) {
+    if (PV_MERKLE_TAIL_ON && m <= (uint64_t)pv::MERKLE_TAIL) {   // the last levels: one launch
+      HIP_OK(pv::launch_merkle_tail(in, m, root, s));
+      break;
+    }
     uint32_t* out = (m + 1) / 2 == 1 ? root : (which ? d.mk1.p : d.mk0.p);
     HIP_OK(pv::launch_merkle_level(in, m, out, s));
     in = out;

@@ -152,6 +152,9 @@ hipError_t sha256_occupancy(int* blocks_per_cu);
 hipError_t launch_sha256(const uint8_t* blob, const uint64_t* off, uint64_t n, uint32_t plen, uint32_t prefix,
                          unsigned long long* counter, uint32_t* out, int blocks, hipStream_t s);
 hipError_t launch_merkle_level(const uint32_t* in, uint64_t m, uint32_t* out, hipStream_t s);
+// the remaining levels of m (2 <= m <= MERKLE_TAIL) nodes in one workgroup -> root
+constexpr int MERKLE_TAIL = 256;
+hipError_t launch_merkle_tail(const uint32_t* in, uint64_t m, uint32_t* root, hipStream_t s);
 
 // deterministic synthetic workload; spec in plenum_gpu/synth.py.
 // mode 0 FIXED (len = mlen_min), 1 RANGE (len uniform in [mlen_min, mlen_max]),

@@ -66,53 +66,108 @@ __device__ __forceinline__ uint64_t wave_append(unsigned long long* counter, uin
   return readlane64(b, leader);
 }
 
-// Wave-private chunks of the global message queue: the wave takes CH indices
-// with one atomic and hands them out to its lanes by ballot rank; the atomic
-// for the NEXT chunk is issued when a chunk is opened and its result is only
-// read (v_readlane of lane 0) when that chunk is exhausted, so no lane ever
-// waits for an atomic round trip (k_hash refilled on nearly every trip on C4
-// and waited for take_index's atomic each time).  Must be called with the
+// Wave-private chunks of the global message queue: the wave takes a chunk of
+// indices with one atomic and hands them out to its lanes by ballot rank; the
+// atomic for the NEXT chunk is issued when a chunk is opened and its result is
+// only read (v_readlane of lane 0) when that chunk is exhausted, so no lane
+// ever waits for an atomic round trip (k_hash refilled on nearly every trip on
+// C4 and waited for take_index's atomic each time).  Must be called with the
 // whole wavefront active (convergent code).
+// Chunk sizes (PV_HASH_GUIDED = 1) follow the batch's mean message length and
+// what is left.  A chunk holds about 16 x 64 blocks of work: 64 x max(1, 16 /
+// (mean blocks per message)) indices (mean from off[0], off[n]), so short
+// messages (C3: one SHA-512 block each -- at a fixed 64, one atomic per wave
+// per trip, all on one counter) take up to 1024 indices per atomic, while long
+// ones (C4: ~17 blocks) keep 64 and the waves' chunks in flight stay in a
+// narrow window of the blob; and never more than (indices left) / (2 x waves
+// of the grid), so the last chunks are 64 and the grid's tail stays one
+// message per lane.  Measured (profiles/r06_ab_hash_chunk.jsonl,
+// r06_ab_hash_guided.jsonl): a fixed 256 cut C3's k_hash 0.62 -> 0.41 ms but
+// made C2's 0.46 -> 0.58 ms (1M / 256 chunks are ~1.3 per wave); sizing by
+// what is left alone (up to 1024 from the start) gave C3 0.42, C2 0.43, f3's
+// leaf kernel 0.41 -> 0.38 ms, but C4 15.1 -> 16.3 ms (every wave streaming
+// its own far-apart MBs of a 17 GB blob); a trip-count estimate of the length
+// misjudged every wave's first chunk.  PV_HASH_GUIDED = 0: fixed chunks of
+// PV_HASH_CHUNK.  k_sha256 keeps fixed chunks (G = false): its f3 leaf kernel
+// (5-block messages) measured 0.41 ms with them and 0.44-0.45 with the sized
+// ones (profiles/r06_ab_f3_queue.jsonl).
 #ifndef PV_HASH_CHUNK
 #define PV_HASH_CHUNK 64
 #endif
+#ifndef PV_HASH_GUIDED
+#define PV_HASH_GUIDED 1
+#endif
 struct WaveQueue {
-  uint64_t cb;    // current chunk base
-  uint32_t cu;    // indices of the current chunk already handed out
-  uint64_t nbv;   // lane 0: base of the next chunk (atomic in flight)
+  uint64_t cb;     // current chunk base
+  uint32_t cs;     // current chunk size
+  uint32_t cu;     // indices of the current chunk already handed out
+  uint64_t nbv;    // lane 0: base of the next chunk (atomic in flight)
+  uint32_t ns;     // size of the next chunk (wave-uniform)
+  uint32_t fit;    // chunk size for the batch's mean message length
+  uint64_t n;      // queue length
+  float rw2;       // 1 / (2 x waves of the grid)
 };
 
-__device__ __forceinline__ void wq_init(WaveQueue& q, unsigned long long* counter) {
+// chunk size for a mean of `blocks` compressions per message
+__device__ __forceinline__ uint32_t wq_fit(uint64_t blocks) {
+  const uint64_t per = 16 / (blocks < 1 ? 1 : blocks);
+  return 64u * (uint32_t)(per < 1 ? 1 : per);
+}
+
+// size of a chunk starting at `base`: q.fit capped by what is left (G), or a
+// fixed PV_HASH_CHUNK
+template <bool G>
+__device__ __forceinline__ uint32_t wq_size(const WaveQueue& q, uint64_t base) {
+  if (G) {
+    const uint64_t left = q.n > base ? q.n - base : 0;
+    uint64_t g = (uint64_t)((float)left * q.rw2) & ~63ull;   // a heuristic: no exact division needed
+    if (g > q.fit) g = q.fit;
+    return (uint32_t)(g < 64 ? 64 : (g > 1024 ? 1024 : g));
+  }
+  return (uint32_t)PV_HASH_CHUNK;
+}
+
+template <bool G>
+__device__ __forceinline__ void wq_init(WaveQueue& q, unsigned long long* counter, uint64_t n, uint32_t fit) {
   const int lane = (int)(threadIdx.x & 63u);
+  q.n = n;
+  q.rw2 = 1.0f / (float)(2u * gridDim.x * (blockDim.x / 64u));
+  q.fit = __builtin_amdgcn_readfirstlane(fit);   // wave-uniform (every lane computed the same value)
+  const uint32_t s0 = wq_size<G>(q, 0);
   unsigned long long b = 0, nb = 0;
   if (lane == 0) {
-    b = atomicAdd(counter, (unsigned long long)PV_HASH_CHUNK);
-    nb = atomicAdd(counter, (unsigned long long)PV_HASH_CHUNK);
+    b = atomicAdd(counter, (unsigned long long)s0);
+    nb = atomicAdd(counter, (unsigned long long)s0);
   }
   q.cb = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
          __builtin_amdgcn_readfirstlane((uint32_t)b);
+  q.cs = s0;
   q.cu = 0;
   q.nbv = nb;
+  q.ns = s0;
 }
 
 // index for every lane with `want` (others get an unused value)
+template <bool G>
 __device__ __forceinline__ uint64_t wq_take(WaveQueue& q, bool want, unsigned long long* counter) {
   const int lane = (int)(threadIdx.x & 63u);
   const uint64_t m = __ballot(want);
   const uint32_t cnt = (uint32_t)__popcll(m);
   const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-  if (q.cu + cnt <= (uint32_t)PV_HASH_CHUNK) {
+  if (q.cu + cnt <= q.cs) {
     const uint64_t idx = q.cb + q.cu + rank;
     q.cu += cnt;
     return idx;
   }
-  const uint32_t first = (uint32_t)PV_HASH_CHUNK - q.cu;
+  const uint32_t first = q.cs - q.cu;
   const uint64_t nb = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(q.nbv >> 32), 0) << 32) |
                       __builtin_amdgcn_readlane((uint32_t)q.nbv, 0);
   const uint64_t idx = rank < first ? q.cb + q.cu + rank : nb + (rank - first);
   q.cb = nb;
-  q.cu = cnt - first;
-  if (lane == 0) q.nbv = atomicAdd(counter, (unsigned long long)PV_HASH_CHUNK);
+  q.cs = q.ns;
+  q.cu = cnt - first;   // <= 64 <= every chunk size
+  q.ns = wq_size<G>(q, nb + q.cs);
+  if (lane == 0) q.nbv = atomicAdd(counter, (unsigned long long)q.ns);
   return idx;
 }
 
@@ -168,8 +223,9 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
   uint32_t ra[16];   // R || A of the current message (block 0's prefix)
   // prefetched next message: offsets, pre-check verdict, R || A
   WaveQueue q;
-  wq_init(q, counter);
-  uint64_t nidx = wq_take(q, true, counter), nmo = 0, nme = 0;
+  // mean SHA-512 blocks per message from the blob's extent
+  wq_init<PV_HASH_GUIDED>(q, counter, n, PV_HASH_GUIDED ? wq_fit(n ? hram_blocks((off[n] - off[0]) / n) : 1) : 64);
+  uint64_t nidx = wq_take<PV_HASH_GUIDED>(q, true, counter), nmo = 0, nme = 0;
   uint32_t nok = 0, nra[16];
   auto prefetch = [&]() {
     if (nidx < n) {
@@ -218,7 +274,7 @@ __global__ __launch_bounds__(HASH_BLOCK, PV_HASH_WAVES) void k_hash(const uint8_
         sha512_init(hs);
       }
     }
-    const uint64_t t = wq_take(q, promote, counter);
+    const uint64_t t = wq_take<PV_HASH_GUIDED>(q, promote, counter);
     if (promote) {
       nidx = t;
       prefetch();
@@ -1285,16 +1341,16 @@ __global__ __launch_bounds__(256) void k_sha256(const uint8_t* __restrict__ blob
                                                  uint64_t n, uint32_t plen, uint32_t prefix,
                                                  unsigned long long* __restrict__ counter, uint32_t* __restrict__ out) {
   WaveQueue q;
-  wq_init(q, counter);
+  wq_init<false>(q, counter, n, 64);
   uint64_t idx = n, blk = 0, nblk = 0, mo = 0, ml = 0;
-  uint64_t nidx = wq_take(q, true, counter), nmo = 0, nme = 0;
+  uint64_t nidx = wq_take<false>(q, true, counter), nmo = 0, nme = 0;
   if (nidx < n) {
     nmo = off[nidx];
     nme = off[nidx + 1];
   }
   uint32_t hs[8];
 #if PV_SHA256_PREFETCH
-  uint32_t y[17];   // the window of the block this lane compresses next
+  uint32_t y[SHA256_Y];   // the window of the block this lane compresses next
   if (nidx < n) sha256_window(y, blob + nmo, nme - nmo, plen, 0);
 #endif
   while (true) {
@@ -1307,7 +1363,7 @@ __global__ __launch_bounds__(256) void k_sha256(const uint8_t* __restrict__ blob
       blk = 0;
       sha256_init(hs);
     }
-    const uint64_t t = wq_take(q, promote, counter);
+    const uint64_t t = wq_take<false>(q, promote, counter);
     if (promote) {
       nidx = t;
       if (nidx < n) {
@@ -1374,6 +1430,47 @@ hipError_t launch_merkle_level(const uint32_t* in, uint64_t m, uint32_t* out, hi
   const uint64_t outs = (m + 1) / 2;
   if (outs == 0) return hipSuccess;
   hipLaunchKernelGGL(k_merkle_level, dim3((uint32_t)((outs + 255) / 256)), dim3(256), 0, s, in, m, out);
+  return hipGetLastError();
+}
+
+// the last levels of a tree in ONE workgroup: m <= MERKLE_TAIL nodes staged in
+// LDS, one node per thread and level, a barrier between levels (replaces one
+// launch per level below MERKLE_TAIL nodes; same pairing and odd-node rule).
+// Measured: from 2048 nodes on one CU the 1024- and 512-node levels ran slower
+// than their own multi-block launches (profiles/r06_ab_merkle_tail.jsonl)
+static_assert(MERKLE_TAIL <= 512, "k_merkle_tail: one node per thread of 256 and level");
+__global__ __launch_bounds__(256) void k_merkle_tail(const uint32_t* __restrict__ in, uint32_t m,
+                                                       uint32_t* __restrict__ root) {
+  __shared__ uint32_t lv[MERKLE_TAIL * 8];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 8 * m; i += 256) lv[i] = in[i];
+  __syncthreads();
+  while (m > 1) {
+    const uint32_t half = m / 2;
+    uint32_t h[8];
+    if (tid < half) {
+      uint32_t lr[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) lr[k] = lv[16 * tid + k];
+      sha256_node(h, lr);
+    } else if (tid == half && (m & 1)) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h[k] = lv[8 * (m - 1) + k];
+    }
+    __syncthreads();
+    if (tid < half || (tid == half && (m & 1))) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) lv[8 * tid + k] = h[k];
+    }
+    __syncthreads();
+    m = (m + 1) / 2;
+  }
+  if (tid < 8) root[tid] = lv[tid];
+}
+
+hipError_t launch_merkle_tail(const uint32_t* in, uint64_t m, uint32_t* root, hipStream_t s) {
+  if (m < 2 || m > (uint64_t)MERKLE_TAIL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_merkle_tail, dim3(1), dim3(256), 0, s, in, (uint32_t)m, root);
   return hipGetLastError();
 }
 

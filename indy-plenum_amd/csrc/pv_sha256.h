@@ -91,11 +91,78 @@ PV_HD uint32_t funnel32_(uint32_t hi, uint32_t lo, uint32_t sh) {
 PV_HD uint64_t sha256_blocks(uint64_t mlen, uint32_t plen) { return (plen + mlen + 9 + 63) / 64; }
 
 // block `blk` of (prefix || M) as 16 big-endian words, SHA padding and length
-// applied.  Guarded aligned loads: the blob needs >= 16 readable bytes after the
-// last message.
+// applied, from the aligned-word window of its first data byte.
+// PV_SHA256_GROUPS = 1: the window is fetched as 4-word groups (group g is
+// loaded iff its first word holds a message byte: at most 5 dwordx4 loads per
+// lane and block instead of 17 guarded dword loads, each of which touches one
+// cache line per lane; a group reads at most 15 bytes past the message end, so
+// the blob needs >= 16 readable bytes after the last message), and the padding
+// is branch-free 32-bit selects (the clamped terminator position, as
+// msg_assemble of pv_verify_core.h); 0 = the per-word form (A/B baseline).
+#ifndef PV_SHA256_GROUPS
+#define PV_SHA256_GROUPS 1
+#endif
+#if PV_SHA256_GROUPS
+constexpr int SHA256_Y = 20;
+PV_HD void sha256_window(uint32_t y[SHA256_Y], const uint8_t* m, uint64_t mlen, uint32_t plen, uint64_t blk) {
+  const bool pre = plen != 0 && blk == 0;
+  const uint64_t q = pre ? 0 : 64 * blk - plen;        // first data byte of the window
+  const int64_t rem = (int64_t)mlen - (int64_t)q;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(m) + q;
+  const uint32_t mis = (uint32_t)(base & 3u);
+  const uint32_t* wp = reinterpret_cast<const uint32_t*>(m + q - mis);
+#pragma unroll
+  for (int g = 0; g < 5; ++g) {
+    uint32_t a = 0, b = 0, c = 0, d = 0;
+    if ((int64_t)(16 * g) - (int64_t)mis < rem) {
+      a = wp[4 * g];
+      b = wp[4 * g + 1];
+      c = wp[4 * g + 2];
+      d = wp[4 * g + 3];
+    }
+    y[4 * g] = a;
+    y[4 * g + 1] = b;
+    y[4 * g + 2] = c;
+    y[4 * g + 3] = d;
+  }
+}
+PV_HD void sha256_assemble(uint32_t w[16], const uint32_t y[SHA256_Y], const uint8_t* m, uint64_t mlen, uint32_t plen,
+                           uint32_t prefix, uint64_t blk, uint64_t nblk) {
+  const bool pre = plen != 0 && blk == 0;
+  const uint64_t q = pre ? 0 : 64 * blk - plen;
+  const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(m) + q) & 3u);
+  uint32_t d[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) d[k] = funnel32_(y[k + 1], y[k], 8u * mis);
+  if (pre) {  // shift the data one byte up and put the prefix in byte 0
+#pragma unroll
+    for (int k = 15; k > 0; --k) d[k] = funnel32_(d[k], d[k - 1], 24u);
+    d[0] = (d[0] << 8) | (prefix & 0xffu);
+  }
+  // terminator position in this block, clamped to [-1, 68]: words below it
+  // are data, the word holding it keeps its low t % 4 bytes and takes 0x80,
+  // words above it are zero
+  const int64_t t64 = (int64_t)(plen + mlen) - (int64_t)(64 * blk);
+  const int32_t t = t64 < 0 ? -1 : (t64 > 68 ? 68 : (int32_t)t64);
+  const uint32_t rb = 8u * ((uint32_t)t & 3u);
+  const uint32_t keep = (1u << rb) - 1u, pad = 0x80u << rb;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t v = d[k];
+    const uint32_t tv = (v & keep) | pad;
+    w[k] = bswap32_(t >= 4 * k + 4 ? v : (t >= 4 * k ? tv : 0u));
+  }
+  if (blk + 1 == nblk) {
+    const uint64_t bits = (plen + mlen) * 8;
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+  }
+}
+#else
+constexpr int SHA256_Y = 17;
 // the aligned-word window of block blk of (prefix || M): 17 words from the
 // aligned-down first data byte, zero past the message (no load issued there)
-PV_HD void sha256_window(uint32_t y[17], const uint8_t* m, uint64_t mlen, uint32_t plen, uint64_t blk) {
+PV_HD void sha256_window(uint32_t y[SHA256_Y], const uint8_t* m, uint64_t mlen, uint32_t plen, uint64_t blk) {
   const bool pre = plen != 0 && blk == 0;
   const uint64_t q = pre ? 0 : 64 * blk - plen;        // first data byte of the window
   const int64_t rem = (int64_t)mlen - (int64_t)q;
@@ -107,7 +174,7 @@ PV_HD void sha256_window(uint32_t y[17], const uint8_t* m, uint64_t mlen, uint32
 }
 // block blk's 16 big-endian words from its window: funnel shift by the
 // misalignment, the prefix byte, the 0x80 terminator and the bit length
-PV_HD void sha256_assemble(uint32_t w[16], const uint32_t y[17], const uint8_t* m, uint64_t mlen, uint32_t plen,
+PV_HD void sha256_assemble(uint32_t w[16], const uint32_t y[SHA256_Y], const uint8_t* m, uint64_t mlen, uint32_t plen,
                            uint32_t prefix, uint64_t blk, uint64_t nblk) {
   const bool pre = plen != 0 && blk == 0;
   const uint64_t q = pre ? 0 : 64 * blk - plen;
@@ -137,9 +204,10 @@ PV_HD void sha256_assemble(uint32_t w[16], const uint32_t y[17], const uint8_t* 
     w[15] = (uint32_t)bits;
   }
 }
+#endif
 PV_HD void sha256_block(uint32_t w[16], const uint8_t* m, uint64_t mlen, uint32_t plen, uint32_t prefix, uint64_t blk,
                         uint64_t nblk) {
-  uint32_t y[17];
+  uint32_t y[SHA256_Y];
   sha256_window(y, m, mlen, plen, blk);
   sha256_assemble(w, y, m, mlen, plen, prefix, blk, nblk);
 }

@@ -623,6 +623,10 @@ constexpr int KEY_WORDS = KEY_STATUS + 32;   // status word + padding: every key
 // so k_keys lays it out lane-interleaved ([word][lane] per 64 keys: every
 // scratch load and store of a wave is one contiguous 256-byte row); only the
 // final affine entries go to the key-major table the curve kernel reads.
+// PV_KEYS_XYP = 1 (A/B): the prefix products folded into X and Y, see key_prepare
+#ifndef PV_KEYS_XYP
+#define PV_KEYS_XYP 0
+#endif
 constexpr int KS_XYZ = 0;
 constexpr int KS_PREFIX = 8 * COMB_Q * 30;
 constexpr int KEY_SCRATCH = KS_PREFIX + 8 * COMB_Q * 10;
@@ -678,6 +682,33 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
     ge_cached c1;
     ge_p3_to_cached(c1, P);
     ge_p3 Q = P;
+#if PV_KEYS_XYP
+    // (A/B) X P_(e-1), Y P_(e-1), Z per entry: 30 scratch words instead of
+    // 40, one more multiply per entry (backward: x = X' acc, y = Y' acc)
+    auto put = [&](int e, const ge_p3& R) {
+      if (e == 0) {
+        store_fe<LS>(xyz(e), R.X);
+        store_fe<LS>(xyz(e) + 10 * LS, R.Y);
+        fe_copy(zacc, R.Z);
+      } else {
+        fe t;
+        fe_mul(t, R.X, zacc);
+        store_fe<LS>(xyz(e), t);
+        fe_mul(t, R.Y, zacc);
+        store_fe<LS>(xyz(e) + 10 * LS, t);
+        fe_mul(zacc, zacc, R.Z);
+      }
+      store_fe<LS>(xyz(e) + 20 * LS, R.Z);
+    };
+    put(8 * q, Q);
+#pragma unroll 1
+    for (int k = 2; k <= 8; ++k) {
+      ge_p1p1 t;
+      ge_add_cached(t, Q, c1, false);
+      ge_p1p1_to_p3(Q, t);
+      put(8 * q + k - 1, Q);
+    }
+#else
     store_fe<LS>(xyz(8 * q), Q.X);
     store_fe<LS>(xyz(8 * q) + 10 * LS, Q.Y);
     store_fe<LS>(xyz(8 * q) + 20 * LS, Q.Z);
@@ -698,6 +729,7 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
       fe_mul(zacc, zacc, Q.Z);
       store_fe<LS>(pre(e), zacc);
     }
+#endif
     if (q + 1 < COMB_Q) {  // A_{q+1} = 2^32 A_q = 2^29 (8 A_q)
       ge_p1p1 t;
       ge_p2 r;
@@ -721,7 +753,9 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
   fe_invert(acc, zacc);
   fe d2;
   fe_const_d2(d2);
+#if !PV_KEYS_XYP
   load_fe<LS>(un, pre(NE - 2));
+#endif
   load_fe<LS>(xn, xyz(NE - 1));
   load_fe<LS>(yn, xyz(NE - 1) + 10 * LS);
   load_fe<LS>(zn, xyz(NE - 1) + 20 * LS);
@@ -733,11 +767,19 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
     fe_copy(x, xn);
     fe_copy(y, yn);
     if (e > 0) {
+#if !PV_KEYS_XYP
       if (e > 1) load_fe<LS>(un, pre(e - 2));
+#endif
       load_fe<LS>(xn, xyz(e - 1));
       load_fe<LS>(yn, xyz(e - 1) + 10 * LS);
       load_fe<LS>(zn, xyz(e - 1) + 20 * LS);
     }
+#if PV_KEYS_XYP
+    // acc = (Z_0 ... Z_e)^-1 and X' = X P_(e-1): x = X' acc = X / Z_e
+    fe_mul(x, x, acc);
+    fe_mul(y, y, acc);
+    if (e > 0) fe_mul(acc, acc, z);  // (Z_0 ... Z_{e-1})^-1
+#else
     fe zi;
     if (e > 0) {
       fe_mul(zi, acc, u);            // Z_e^-1
@@ -747,6 +789,7 @@ PV_HD void key_prepare(uint32_t* kt, uint32_t* scr, const uint8_t* pk) {
     }
     fe_mul(x, x, zi);
     fe_mul(y, y, zi);
+#endif
     fe ypx, ymx;
     fe_add(ypx, y, x); fe_carry(ypx);
     fe_sub(ymx, y, x); fe_carry(ymx);

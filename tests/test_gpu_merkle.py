@@ -107,8 +107,9 @@ def test_full_size_root_and_device_path():
     nat._check('pv_merkle_root_device', nat.load().pv_merkle_root_device(_p(blob), _p(off), n, _p(None), _p(root), 0,
                                                                          _stream(dev)))
     assert bytes(root.cpu().numpy()) == want
-    # odd sizes through the device path too
-    for m in (1, 2, 3, 1023, 1025):
+    # odd sizes through the device path too, either side of the one-workgroup
+    # tail (k_merkle_tail takes over at <= 256 nodes)
+    for m in (1, 2, 3, 255, 256, 257, 1023, 1025, 2047, 2049, 4097, 6001):
         nat._check('pv_merkle_root_device', nat.load().pv_merkle_root_device(_p(blob), _p(off), m, _p(None), _p(root),
                                                                              0, _stream(dev)))
         assert bytes(root.cpu().numpy()) == mk.mth_levelwise(leaves[:m]), m
