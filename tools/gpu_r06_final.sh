@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 closing evidence on the current build: the -m gpu suite and smoke(),
 # the default bench line (C2 + every other config), rocprofv3 kernel stats of
-# the C2 / C4 lines run sequentially (the roofline's kernel durations) and of the
+# the C2 / C4 / C3 lines run sequentially (the roofline's kernel durations) and of the
 # C3-BLS line.  Each GPU step under its own limit; the chain stops at a failure.
 #   bash tools/gpu_r06_final.sh OUT
 set -u
@@ -20,6 +20,9 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/c2_seq" -o run -- py
 echo "[final] $(date +%T) stats c4" && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/c4_seq" -o run -- python3 bench.py --config c4 --sequential \
     --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > "$out/c4_seq.json" 2> "$out/c4_seq.err" && \
+echo "[final] $(date +%T) stats c3" && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/c3_seq" -o run -- python3 bench.py --config c3 --sequential \
+    --steps 5 --warmup 1 --no-cpu-baseline --no-e2e > "$out/c3_seq.json" 2> "$out/c3_seq.err" && \
 echo "[final] $(date +%T) stats c3bls" && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/c3bls" -o run -- python3 bench.py --config c3bls \
     --steps 3 --warmup 1 --no-cpu-baseline > "$out/c3bls.json" 2> "$out/c3bls.err" && echo "[final] done"
