@@ -333,3 +333,12 @@ def test_async_slot_rejected(torch_dev):
     rc = nat.load().pv_verify_batch_device_async(_p(b.pk), _p(b.sig), _p(b.blob), _p(b.off), b.n, _p(b.verdict),
                                                  _p(b.bitmap), 0, s, 2)
     assert rc != 0
+    # the one-call key preparation + keyed verify: bad slot, bad format, signatures without keys
+    import torch
+    kt = torch.empty(nat.PV_KEY_WORDS, dtype=torch.int32, device=b.device)
+    ki = torch.zeros(b.n, dtype=torch.int32, device=b.device)
+    lib = nat.load()
+    for k, wide, slot in ((1, 0, 2), (1, 2, 0), (0, 0, 0)):
+        rc = lib.pv_verify_keys_device_async(_p(b.pk), k, _p(kt), _p(ki), _p(b.sig), _p(b.blob), _p(b.off), b.n,
+                                             _p(b.verdict), _p(b.bitmap), wide, 0, s, slot)
+        assert rc != 0, (k, wide, slot)
