@@ -207,7 +207,8 @@ int pv_verify_keyed_wide_device_async(const uint32_t *ktab, const uint32_t *key_
  * verdicts and tables as
  * pv_keys_prepare[_wide]_device_async followed by
  * pv_verify_keyed[_wide]_device_async on the same stream, which run the two
- * stages one after the other.  n = 0 only prepares the keys. */
+ * stages one after the other.  n = 0 only prepares the keys.  As for every
+ * keyed call, each key_idx[i] must be < k: the kernels do not bound-check it. */
 int pv_verify_keys_device_async(const uint8_t *pk, uint64_t k, uint32_t *ktab, const uint32_t *key_idx,
                                 const uint8_t *sig, const uint8_t *msg_blob, const uint64_t *msg_off, uint64_t n,
                                 uint8_t *verdict, uint64_t *bitmap, uint32_t wide, int device, void *stream, int slot);
